@@ -1,0 +1,114 @@
+/*
+ * sqr.h — C ABI of libsqr.so, the MI355X (gfx950) hot path of sq-recovery.
+ *
+ * Every entry point is a plain C function over plain pointers and sizes (no
+ * torch types).  Conventions for all calls:
+ *   - pointers are DEVICE pointers owned by the caller; the library allocates
+ *     nothing and never synchronises the host;
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream);
+ *     kernels are enqueued on it, so calls are graph-capturable;
+ *   - return 0 on success, otherwise a negative SQR_E* code or a positive
+ *     hipError_t; sqr_last_error_string() describes the last failure on the
+ *     calling thread.
+ *
+ * Reference interfaces replaced (timoblak/sq-recovery, file:line):
+ *   sqr_implicit_loss_fwd_bwd  torch/classes.py:203-295  ImplicitLoss (__init__ grid :217-222,
+ *                              preprocess_sq :224-230, depth_projection :232-282, __call__ :284-295)
+ *                              + its autograd backward (analytic here)
+ *   sqr_implicit_render        torch/classes.py:232-282  ImplicitLoss.depth_projection (forward only)
+ *   sqr_explicit_loss_fwd_bwd  torch/classes.py:109-201  ExplicitLoss (occupancy :138-189, __call__ :191-201)
+ *   sqr_iou_counts             torch/classes.py:374-447  IoUAccuracy (ins_outs :394-426, __call__ :428-447)
+ *   sqr_conv2d_fwd / _bwd_data / _bwd_weight
+ *                              torch.nn.Conv2d as used by torchvision resnet18 inside ResNetSQ
+ *                              (torch/models.py:181-184) and by GenericNetSQ (torch/models.py:134-152)
+ *                              — forward and the two autograd backward products.
+ */
+#ifndef SQR_H
+#define SQR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes (negative; positive values are hipError_t) */
+#define SQR_OK 0
+#define SQR_E_INVALID_ARG (-1)
+#define SQR_E_UNSUPPORTED (-2)
+#define SQR_E_WORKSPACE (-3)
+
+/* element types for the conv entry points */
+#define SQR_DTYPE_F32 0
+#define SQR_DTYPE_BF16 1
+
+int sqr_version(void);
+const char* sqr_last_error_string(void);
+
+/* ---------------------------------------------------------------- losses */
+
+/* Workspace (bytes, device) needed by sqr_implicit_loss_fwd_bwd for B samples at render size R. */
+size_t sqr_implicit_loss_workspace_bytes(int B, int R);
+
+/* ImplicitLoss(R, tau, sharpness)(target, params) and d loss / d params.
+ *   params  [B,12] f32 : a(3) e(2) t(3) q(4, xyzw) — raw network output (clamped inside)
+ *   target  [B,H,W] f32 : the depth image (channel dim squeezed); nearest-resampled to RxR
+ *   loss_per_sample [B] f64 : mean_{r,c} |target_resized - render|; the reference loss is their mean
+ *   grad_params [B,12] f32 : d(mean_b loss_b)/d params   (written only when need_grad != 0)
+ * 2 <= R <= 256 when need_grad, R >= 2 otherwise; H,W >= 1. */
+int sqr_implicit_loss_fwd_bwd(const float* params, const float* target, int B, int H, int W, int R,
+                              float tau, float sharpness, int need_grad, double* loss_per_sample,
+                              float* grad_params, void* workspace, size_t workspace_bytes, void* stream);
+
+/* depth_projection only: images [B,R,R] f32 in the reference's image orientation (row = R-1-y, col = x). */
+int sqr_implicit_render(const float* params, int B, int R, float tau, float sharpness, float* images,
+                        void* stream);
+
+size_t sqr_explicit_loss_workspace_bytes(int B, int R);
+
+/* ExplicitLoss(R)(p_true, p_pred): loss_per_sample [B] f64 = 100*mean (occ_true-occ_pred)^2 on the
+ * (n)^3 grid, n = len(arange(0, 1+1/R, 1/R)); grad_pred [B,12] f32 = d(mean_b loss_b)/d p_pred. */
+int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pred, int B, int R, int need_grad,
+                              double* loss_per_sample, float* grad_pred, void* workspace,
+                              size_t workspace_bytes, void* stream);
+
+/* IoUAccuracy(R): per-sample voxel counts [B,2] int64 = (|in_true & in_pred|, |in_true | in_pred|),
+ * computed in float64 like the reference. */
+int sqr_iou_counts(const float* p_true, const float* p_pred, int B, int R, long long* counts,
+                   void* stream);
+
+/* ---------------------------------------------------------------- conv2d (implicit GEMM, NHWC) */
+
+/* Activations are NHWC (torch channels_last), weights KRSC for fwd/wgrad and CRSK for dgrad
+ * (sqr_conv2d_pack_weight produces both from torch's KCRS fp32 master weight).
+ * dtype SQR_DTYPE_BF16: bf16 in/out, fp32 accumulation (MFMA 16x16x32 bf16).
+ * dtype SQR_DTYPE_F32 : f32 in/out, exact-f32 MFMA (16x16x4 f32) — the parity mode. */
+typedef struct sqr_conv_desc {
+  int N, C, H, W;   /* input */
+  int K, R, S;      /* filters */
+  int stride, pad;  /* symmetric */
+  int dtype;        /* SQR_DTYPE_* */
+} sqr_conv_desc;
+
+int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo);
+size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which /*0 fwd,1 dgrad,2 wgrad*/);
+
+/* w_kcrs f32 [K,C,R,S] -> w_krsc [K,R,S,Cp] and (optionally) w_crsk [C,R,S,K] in d->dtype.
+ * Cp = C rounded up to 8 (zero-padded) so the channel dim is 16-byte vectorisable. */
+int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* d, void* w_krsc, void* w_crsk,
+                           void* stream);
+/* x [N,H,W,Cp] (Cp = C rounded up to 8), y [N,Ho,Wo,K] */
+int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, void* workspace,
+                   size_t workspace_bytes, void* stream);
+/* dy [N,Ho,Wo,K], w_crsk [C,R,S,K] -> dx [N,H,W,C] */
+int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
+                        void* workspace, size_t workspace_bytes, void* stream);
+/* x [N,H,W,Cp], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
+int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SQR_H */

@@ -1,0 +1,86 @@
+"""ctypes binding of libsqr.so (the C ABI declared in include/sqr.h).
+
+The library is built in-tree (``make -C sq-recovery_amd/csrc`` or ``__graft_entry__.build()``)
+into this directory.  There is no fallback: if the library is missing, ``lib()`` raises, so a
+GPU run can never silently take another code path.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (loads torch's libamdhip64 first; libsqr binds to that runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SQR_LIB", os.path.join(_HERE, "libsqr.so"))
+
+_lock = threading.Lock()
+_lib = None
+
+c_int, c_float, c_double, c_size_t, c_void_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
+                                                ctypes.c_size_t, ctypes.c_void_p)
+
+
+class SqrConvDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("N", "C", "H", "W", "K", "R", "S", "stride", "pad", "dtype")]
+
+
+# name -> (restype, argtypes); must mirror include/sqr.h exactly
+SIGNATURES = {
+    "sqr_version": (c_int, []),
+    "sqr_last_error_string": (ctypes.c_char_p, []),
+    "sqr_implicit_loss_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "sqr_implicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float,
+                                          c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_implicit_render": (c_int, [c_void_p, c_int, c_int, c_float, c_float, c_void_p, c_void_p]),
+    "sqr_explicit_loss_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "sqr_explicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                          c_void_p, c_size_t, c_void_p]),
+    "sqr_iou_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sqr_conv2d_out_hw": (c_int, [ctypes.POINTER(SqrConvDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "sqr_conv2d_workspace_bytes": (c_size_t, [ctypes.POINTER(SqrConvDesc), c_int]),
+    "sqr_conv2d_pack_weight": (c_int, [c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_void_p, c_void_p]),
+    "sqr_conv2d_fwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t,
+                               c_void_p]),
+    "sqr_conv2d_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
+                                    c_size_t, c_void_p]),
+    "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
+                                      c_size_t, c_void_p]),
+}
+
+
+class SqrError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if libsqr.so is absent or incomplete."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise SqrError("libsqr.so not found at %s — build it with `make -C sq-recovery_amd/csrc` "
+                           "(or __graft_entry__.build()); there is no fallback path" % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)  # AttributeError = library/header mismatch: fail loudly
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().sqr_last_error_string().decode(errors="replace")
+        raise SqrError("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def stream_ptr(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return c_void_p(t.data_ptr()) if t is not None else c_void_p(0)

@@ -1,0 +1,37 @@
+"""The C-ABI library: it loads (no GPU needed) and exports every symbol include/sqr.h declares."""
+import os
+import re
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "sqr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sqr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    for s in ("sqr_implicit_loss_fwd_bwd", "sqr_explicit_loss_fwd_bwd", "sqr_iou_counts", "sqr_conv2d_fwd",
+              "sqr_conv2d_bwd_data", "sqr_conv2d_bwd_weight", "sqr_last_error_string"):
+        assert s in syms
+
+
+def test_library_loads_and_exports_all_symbols():
+    from sqr import _lib
+    L = _lib.lib()
+    for s in declared_symbols():
+        assert hasattr(L, s), s
+    assert set(declared_symbols()) == set(_lib.SIGNATURES)
+    assert L.sqr_version() >= 1
+
+
+def test_argument_validation_without_gpu():
+    # invalid arguments are rejected on the host before any HIP call
+    from sqr import _lib
+    L = _lib.lib()
+    rc = L.sqr_implicit_loss_fwd_bwd(None, None, 0, 256, 256, 32, 1.0, 100.0, 1, None, None, None, 0, None)
+    assert rc == -1
+    assert b"B=0" in L.sqr_last_error_string()
+    assert L.sqr_implicit_loss_workspace_bytes(4, 32) == 4 * 4 * 18 * 4
