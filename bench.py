@@ -1,0 +1,208 @@
+"""Training throughput of the sq-recovery hot path on MI355X (BASELINE.json metric).
+
+One step = torch/train.py's step (train.py:86-103) on a synthetic batch: ResNetSQ forward (HIP
+implicit-GEMM convs, bf16 autocast), ImplicitLoss(32, tau=1.5, s=260) on the input depth images
+(fused HIP loss + analytic grad, fp32), backward, Adam(lr=1e-4) step — plus, for N>1, DDP's
+bucketed RCCL all-reduce of the gradients overlapped with backward.  Per-GPU batch 64
+(BASELINE config 2; config 3 = 8 GPUs x 64).
+
+Synthetic data: SQ parameters drawn from the reference's generator distribution
+(gen_rand_rot.py:21-31) with seed 1234+rank, rendered on the GPU into 256x256 depth images with
+the same inside-outside model (values in [0,1], background 0).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sq-recovery_amd"))
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+
+# dominant kernel (largest share of step time in profiles/): the layer1 3x3 64->64 convs
+PROBE = ("wgrad", 64, 64, 3, 1)  # phase, C, H(=W), R, stride  (N = per-GPU batch)
+
+
+def synth_params(rng, n):
+    a = rng.uniform(25, 75, (n, 3)) / 255.0
+    e = rng.uniform(0.1, 1.0, (n, 2))
+    t = (128.0 + rng.uniform(-40, 40, (n, 3))) / 255.0
+    u = rng.uniform(0, 1, (n, 3))
+    q = np.stack([np.sqrt(1 - u[:, 0]) * np.sin(2 * np.pi * u[:, 1]), np.sqrt(1 - u[:, 0]) * np.cos(2 * np.pi * u[:, 1]),
+                  np.sqrt(u[:, 0]) * np.sin(2 * np.pi * u[:, 2]), np.sqrt(u[:, 0]) * np.cos(2 * np.pi * u[:, 2])], 1)
+    return np.concatenate([a, e, t, q], 1).astype(np.float32)
+
+
+def conv_flops(N, C, H, K, R, stride):
+    pad = R // 2
+    Ho = (H + 2 * pad - R) // stride + 1
+    return 2.0 * N * Ho * Ho * K * C * R * R
+
+
+def cpu_baseline(images_cpu, state_dict, R, steps):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_torch
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    net = ref_torch.ResNetSQRef()
+    missing = net.load_state_dict(state_dict, strict=False)
+    assert not missing.missing_keys, missing.missing_keys
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    crit = ref_torch.ImplicitLossRef(R, 1.5, 260)
+    ref_torch.train_step(net, opt, crit, images_cpu)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ref_torch.train_step(net, opt, crit, images_cpu)
+    dt = time.perf_counter() - t0
+    return images_cpu.shape[0] * steps / dt, dt
+
+
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--render", type=int, default=32, help="ImplicitLoss render size R")
+    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline steps (0 = skip)")
+    ap.add_argument("--breakdown", action="store_true", help="print a per-phase timing breakdown to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import classes
+    import models
+    from sqr import conv as sconv
+    from sqr import losses
+
+    B, R, H = args.batch, args.render, 256
+    rng = np.random.default_rng(1234 + rank)
+    params = torch.tensor(synth_params(rng, B), device=dev)
+    images = losses.implicit_render(params, H, 1.5, 260).unsqueeze(1).contiguous()  # [B,1,256,256] in [0,1]
+
+    torch.manual_seed(0)  # identical init on every rank (DDP also broadcasts)
+    net = models.ResNetSQ(outputs=4, pretrained=False).to(dev)
+    state0 = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    model = net
+    if world > 1:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        model = DDP(net, device_ids=[local], bucket_cap_mb=16, gradient_as_bucket_view=True,
+                    broadcast_buffers=False)
+    try:
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0, fused=True)
+    except Exception:
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0)
+    crit = classes.ImplicitLoss(R, dev, 1.5, 260)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(images)
+        pred = torch.cat([o.float() for o in out], dim=1)
+        loss = crit(images, pred)
+        loss.backward()
+        opt.step()
+        return loss.detach()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+
+    pc, ph, pr, ps = PROBE[1], PROBE[2], PROBE[3], PROBE[4]
+    sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
+    loss_acc = torch.zeros((), dtype=torch.float64, device=dev)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss_acc += step()
+    barrier()
+    dt = time.perf_counter() - t0
+    events = sconv.probe_events()
+    sconv.set_probe(None, 0, 0, 0, 0, 0, 0)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    mean_loss = (loss_acc / args.steps).item()
+
+    if args.breakdown and rank == 0:
+        # forward / backward / optimizer split (separate, synchronised run)
+        def timed(fn, n=5):
+            torch.cuda.synchronize()
+            s = time.perf_counter()
+            for _ in range(n):
+                fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - s) / n * 1e3
+        def fwd():
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                model(images)
+        print("breakdown ms: step %.3f fwd(no-grad) %.3f" % (timed(step), timed(fwd)), file=sys.stderr)
+
+    value = B * world * args.steps / dt
+    flops = conv_flops(B, pc, ph, pc, pr, ps)
+    achieved = flops / (kern_ms * 1e-3) / 1e12 if events else None
+    roof = {"bound": "mfma", "kernel": "conv_%s %dx%d %dx%d s%d (layer1, bf16)" % (PROBE[0], pc, pc, pr, pr, ps),
+            "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
+            "kernel_ms": kern_ms, "launches": len(events), "traffic": None}
+    tr = load_traffic()
+    if tr and tr.get("kernel_key") == list(PROBE):
+        roof["traffic"] = tr.get("hbm_bytes_per_launch")
+
+    out = {"metric": "training images/sec (256x256 depth, implicit loss)", "value": value, "unit": "images/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic (GPU-rendered SQ depth images, reference label distribution)",
+           "config": {"workload": "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
+                      "model": "ResNetSQ (resnet18 backbone, 11.37M params)", "global_batch": B * world,
+                      "per_gpu_batch": B, "image": "256x256x1", "render_size": R,
+                      "parallelism": "dp%d" % world},
+           "mean_loss": mean_loss, "roofline": roof}
+
+    if rank == 0 and world == 1 and args.cpu_steps > 0:
+        imgs_cpu = images.detach().cpu()
+        v, secs = cpu_baseline(imgs_cpu, state0, R, args.cpu_steps)
+        out["cpu_baseline"] = {"value": v, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": "%d train steps (1 warm-up) of batch %d: oracle/ref_torch.py ResNetSQ "
+                                         "fp32 + reference-style f64 ImplicitLoss(R=%d), Adam; %.1f s"
+                                         % (args.cpu_steps, B, R, secs)}
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

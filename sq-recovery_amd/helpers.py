@@ -1,0 +1,226 @@
+"""Drop-in for torch/helpers.py (timoblak/sq-recovery): checkpoints, label parsing, scanner
+command lines and plotting utilities.
+
+Checkpoint format is the reference's (helpers.py:42-68):
+    {'epoch', 'model_state_dict', 'optimizer_state_dict', 'loss'}
+with un-prefixed state-dict keys; a DistributedDataParallel model is unwrapped before saving, so
+single-GPU and 8-GPU runs write interchangeable files.  Plotting helpers import matplotlib and
+the scanner helpers cv2 lazily (neither is needed on the training path).
+"""
+import os
+from time import sleep
+
+import numpy as np
+import torch
+
+
+def norm_img(img):
+    img = img - img.min()
+    return img / img.max()
+
+
+def quat2mat(q):
+    """helpers.py:17-24: rotation matrix of the NORMALISED quaternion (xyzw)."""
+    q = np.asarray(q, dtype=np.float64)
+    x, y, z, w = q / np.sqrt(np.square(q).sum())
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def get_command(scanner_loc, fn, params):
+    """helpers.py:27-39: `scanner out.bmp a1 a2 a3 e1 e2 px py pz r11..r33` command line."""
+    params = np.asarray(params)
+    vals = list(params[:3]) + list(params[3:5]) + list(np.ravel(params[5:8])) + list(np.ravel(params[8:]))
+    return scanner_loc + "scanner " + fn + " " + "".join("%f " % v for v in vals) + "\n"
+
+
+def _unwrap(model):
+    return model.module if hasattr(model, "module") and isinstance(model.module, torch.nn.Module) else model
+
+
+def save_model(path, epoch, model, optimizer, loss):
+    """helpers.py:42-48."""
+    torch.save({"epoch": epoch, "model_state_dict": _unwrap(model).state_dict(),
+                "optimizer_state_dict": optimizer.state_dict(), "loss": loss}, path)
+
+
+def _safe_load(path, map_location):
+    try:
+        return torch.load(path, map_location=map_location, weights_only=True)
+    except Exception:
+        # reference checkpoints keep numpy float64 running means in 'loss' (train.py:170)
+        import numpy.core.multiarray as ma
+        with torch.serialization.safe_globals([ma.scalar, np.dtype, np.dtypes.Float64DType]):
+            return torch.load(path, map_location=map_location, weights_only=True)
+
+
+def load_model(path, model, optimizer, plot=False):
+    """helpers.py:51-68 (map_location cuda:0 when a GPU is present, as the reference)."""
+    print("Loading model: " + path)
+    dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+    checkpoint = _safe_load(path, dev)
+    _unwrap(model).load_state_dict(checkpoint["model_state_dict"])
+    if optimizer is not None:
+        optimizer.load_state_dict(checkpoint["optimizer_state_dict"])
+    epoch = checkpoint["epoch"]
+    loss = checkpoint["loss"]
+    if plot:
+        from matplotlib import pyplot as plt
+        plt.plot(loss["loss"], label="Loss")
+        plt.plot(loss["val_loss"], label="Validation Loss")
+        plt.title("Progression of loss during training")
+        plt.xlabel("# Epochs")
+        plt.ylabel("Loss")
+        plt.legend()
+        plt.show()
+    return epoch, model, optimizer, loss
+
+
+def _scanner_params(p, clip):
+    M = quat2mat(p[-4:])
+    if clip:
+        return np.concatenate((np.clip(p[:3], 0.05, 1) * 255., np.clip(p[3:5], 0.1, 1), np.clip(p[5:8], 0, 1) * 255,
+                               M.ravel()))
+    return np.concatenate((p[:3] * 255., p[3:5], p[5:8] * 255, M.ravel()))
+
+
+def save_compare_images(params_true, params_pred):
+    """helpers.py:71-81: renders true/predicted SQs with the external `scanner` binary."""
+    for i, (true, pred) in enumerate(zip(params_true, params_pred)):
+        os.system(get_command("../", "examples/" + str(i) + "_true.bmp", _scanner_params(true, False)))
+        os.system(get_command("../", "examples/" + str(i) + "_pred.bmp", _scanner_params(pred, True)))
+
+
+def compare_images(params_true, params_pred, wait=16):
+    """helpers.py:84-100."""
+    import cv2
+    for true, pred in zip(params_true, params_pred):
+        os.system(get_command("../", "true.bmp", _scanner_params(true, False)))
+        os.system(get_command("../", "pred.bmp", _scanner_params(pred, True)))
+        combined = np.hstack([cv2.imread("true.bmp", 0), cv2.imread("pred.bmp", 0)])
+        cv2.imshow("comparison", combined)
+        cv2.waitKey(wait)
+
+
+def change_lr(opt, lr):
+    for g in opt.param_groups:
+        g["lr"] = lr
+
+
+def plot_render(meshgrid, np_array, mode="all", figure=1, lims=(0, 1), eps=0.1):
+    """helpers.py:108-173 (3-D scatter of an occupancy/inside-outside volume)."""
+    from matplotlib import pyplot as plt
+    from mpl_toolkits.mplot3d import Axes3D  # noqa: F401
+    masks = {"all": np_array >= 0, "in": np_array <= 1, "in_inv": np_array > 0.9, "bit": np_array == 1,
+             "shell": (np_array < 1 + eps) & (np_array > 1 - eps)}
+    disp = masks[mode].ravel()
+    v = np_array.ravel()
+    vn = -1 + (v - v.min()) / (v.max() - v.min()) * 2
+    clr = np.array([gray_to_jet(x) for x in vn])
+    clr[:, 3] = np.where(disp, 1.0, 0.2 if mode in ("in", "in_inv") else 0.0)
+    ax = plt.figure(figure).add_subplot(1, 1, 1, projection="3d")
+    ax.scatter(meshgrid[0], meshgrid[1], meshgrid[2], color=clr, marker="o")
+    ax.set(xlim=lims, ylim=lims, zlim=lims)
+
+
+def plot_points(xs, ys, zs, figure=2, lims=(-1, 1), subplot=111):
+    from matplotlib import pyplot as plt
+    ax = plt.figure(figure).add_subplot(subplot, projection="3d")
+    ax.scatter(xs, ys, zs, marker="o")
+    ax.set(xlim=lims, ylim=lims, zlim=lims)
+    ax.set_xlabel("X Axis")
+    ax.set_ylabel("Y Axis")
+    ax.set_zlabel("Z Axis")
+
+
+def parse_csv(csvfile):
+    """helpers.py:188-218: rows 'fn,a1,a2,a3,e1,e2,t1,t2,t3,m11..m33,q1..q4' ->
+    float32 [a/255 (3), e (2), t/255 (3), q (4)] per image."""
+    with open(csvfile, "r") as f:
+        lines = f.read().split("\n")
+    print("Parsing csv " + csvfile)
+    labels = []
+    for line in lines:
+        if line == "":
+            continue
+        v = line.split(",")
+        row = [float(v[i]) / 255.0 if i in (1, 2, 3, 6, 7, 8) else float(v[i]) for i in range(1, 9)]
+        row += [float(v[i]) for i in range(-4, 0)]
+        labels.append(np.array(row, dtype=np.float32))
+    print("Size of data: " + str(len(labels)))
+    print("----------------------------------------------------------------")
+    return labels
+
+
+def gray_to_jet(gray):
+    """helpers.py:221-239: value in [-1,1] -> (r, g, b, a) of the jet colormap."""
+    def base(val):
+        if val <= -0.75:
+            return 0.0
+        if val <= -0.25:
+            return (val + 0.75) / 0.5
+        if val <= 0.25:
+            return 1.0
+        if val <= 0.75:
+            return 1.0 - (val - 0.25) / 0.5
+        return 0.0
+    return base(gray - 0.5), base(gray), base(gray + 0.5), 1
+
+
+def plot_grad_flow(named_parameters):
+    """helpers.py:242-268: bar plot of mean/max |grad| per weight tensor."""
+    from matplotlib import pyplot as plt
+    layers, ave, mx = [], [], []
+    for n, p in named_parameters:
+        if p.requires_grad and "bias" not in n and p.grad is not None:
+            layers.append(n)
+            ave.append(p.grad.abs().mean().item())
+            mx.append(p.grad.abs().max().item())
+    plt.bar(np.arange(len(mx)), mx, alpha=0.1, lw=1, color="c")
+    plt.bar(np.arange(len(mx)), ave, alpha=0.1, lw=1, color="b")
+    plt.xticks(range(len(ave)), layers, rotation="vertical")
+    plt.title("Gradient flow")
+
+
+def getBack(var_grad_fn):
+    """helpers.py:271-283: walk an autograd graph printing leaf gradients."""
+    print(var_grad_fn)
+    for n in var_grad_fn.next_functions:
+        if n[0]:
+            try:
+                sleep(1)
+                tensor = getattr(n[0], "variable")
+                print(n[0])
+                print("Tensor with grad found:", tensor)
+                print(" - gradient:", tensor.grad)
+                print()
+            except AttributeError:
+                getBack(n[0])
+
+
+def randquat():
+    """helpers.py:286-292."""
+    u = np.random.uniform(0, 1, (3,))
+    a, b = np.sqrt(1 - u[0]), np.sqrt(u[0])
+    return np.array([a * np.sin(2 * np.pi * u[1]), a * np.cos(2 * np.pi * u[1]),
+                     b * np.sin(2 * np.pi * u[2]), b * np.cos(2 * np.pi * u[2])])
+
+
+def slerp(v0, v1, t_array):
+    """helpers.py:295-320: spherical linear interpolation."""
+    t_array = np.array(t_array)
+    v0 = np.array(v0)
+    v1 = np.array(v1)
+    dot = np.sum(v0 * v1)
+    if dot < 0.0:
+        v1 = -v1
+        dot = -dot
+    if dot > 0.9995:
+        result = v0[np.newaxis, :] + t_array[:, np.newaxis] * (v1 - v0)[np.newaxis, :]
+        return (result.T / np.linalg.norm(result, axis=1)).T
+    theta_0 = np.arccos(dot)
+    theta = theta_0 * t_array
+    s0 = np.cos(theta) - dot * np.sin(theta) / np.sin(theta_0)
+    s1 = np.sin(theta) / np.sin(theta_0)
+    return (s0[:, np.newaxis] * v0[np.newaxis, :]) + (s1[:, np.newaxis] * v1[np.newaxis, :]), v1

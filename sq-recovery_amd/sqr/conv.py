@@ -1,0 +1,182 @@
+"""nn.Conv2d-compatible convolution on the HIP implicit-GEMM kernels (libsqr sqr_conv2d_*).
+
+Activations are NHWC in memory (torch channels_last); the fp32 master weight stays in torch's
+[K,C,R,S] layout so state-dict keys/shapes are unchanged (torchvision resnet18 / GenericNetSQ,
+torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
+([K,R,S,C] for fwd, [C,R,S,K] for backward-data) in the compute dtype.
+
+Compute dtype: bfloat16 when the input is bf16 or CUDA autocast is on with bf16, else float32
+(exact-f32 MFMA: the parity mode).
+"""
+import torch
+import torch.nn as nn
+
+from ._lib import SqrConvDesc, check, lib, ptr, stream_ptr
+
+DT_F32, DT_BF16 = 0, 1
+_CL = torch.channels_last
+
+# Optional kernel probe (bench.py): HIP events recorded on the launch stream around every launch
+# of one (phase, conv shape), to time that kernel live inside a training step.
+_probe = {"key": None, "events": []}
+
+
+def set_probe(phase, N, C, H, K, R, stride):
+    """phase in {'fwd','dgrad','wgrad'}; shape as the conv's (N, C, H, K, R, stride)."""
+    _probe["key"] = (phase, N, C, H, K, R, stride)
+    _probe["events"] = []
+
+
+def probe_events():
+    return _probe["events"]
+
+
+class _Probe:
+    def __init__(self, phase, d):
+        self.on = _probe["key"] == (phase, d.N, d.C, d.H, d.K, d.R, d.stride)
+
+    def __enter__(self):
+        if self.on:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+    def __exit__(self, *exc):
+        if self.on:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            _probe["events"].append((self.e0, e1))
+
+
+def _desc(N, C, H, W, K, R, S, stride, pad, dtype):
+    return SqrConvDesc(N, C, H, W, K, R, S, stride, pad, DT_BF16 if dtype == torch.bfloat16 else DT_F32)
+
+
+def _out_hw(d):
+    import ctypes
+    ho, wo = ctypes.c_int(), ctypes.c_int()
+    check(lib().sqr_conv2d_out_hw(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo)), "sqr_conv2d_out_hw")
+    return ho.value, wo.value
+
+
+def _ws(d, which, device):
+    import ctypes
+    n = lib().sqr_conv2d_workspace_bytes(ctypes.byref(d), which)
+    return torch.empty(max(n, 16), dtype=torch.uint8, device=device), n
+
+
+def pack_weight(weight, d, need_crsk):
+    import ctypes
+    K, C, R, S = weight.shape
+    dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+    w = weight.detach().to(torch.float32).contiguous()
+    if C < 8:
+        kp = 64
+        while kp < R * S * C:
+            kp *= 2
+        krsc = torch.empty(K, kp, dtype=dt, device=w.device)
+    else:
+        krsc = torch.empty(K, R, S, C, dtype=dt, device=w.device)
+    crsk = torch.empty(C, R, S, K, dtype=dt, device=w.device) if need_crsk else None
+    check(lib().sqr_conv2d_pack_weight(ptr(w), ctypes.byref(d), ptr(krsc), ptr(crsk), stream_ptr(w.device)),
+          "sqr_conv2d_pack_weight")
+    return krsc, crsk
+
+
+def conv2d_fwd(x, w_krsc, d):
+    import ctypes
+    ho, wo = _out_hw(d)
+    dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+    y = torch.empty((d.N, d.K, ho, wo), dtype=dt, device=x.device, memory_format=_CL)
+    ws, n = _ws(d, 0, x.device)
+    with _Probe("fwd", d):
+        rc = lib().sqr_conv2d_fwd(ptr(x), ptr(w_krsc), ptr(y), ctypes.byref(d), ptr(ws), n, stream_ptr(x.device))
+    check(rc, "sqr_conv2d_fwd")
+    return y
+
+
+def conv2d_bwd_data(gy, w_crsk, d):
+    import ctypes
+    dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+    dx = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=gy.device, memory_format=_CL)
+    ws, n = _ws(d, 1, gy.device)
+    with _Probe("dgrad", d):
+        rc = lib().sqr_conv2d_bwd_data(ptr(gy), ptr(w_crsk), ptr(dx), ctypes.byref(d), ptr(ws), n,
+                                       stream_ptr(gy.device))
+    check(rc, "sqr_conv2d_bwd_data")
+    return dx
+
+
+def conv2d_bwd_weight(x, gy, d):
+    import ctypes
+    dw = torch.empty((d.K, d.C, d.R, d.S), dtype=torch.float32, device=x.device)
+    ws, n = _ws(d, 2, x.device)
+    with _Probe("wgrad", d):
+        rc = lib().sqr_conv2d_bwd_weight(ptr(x), ptr(gy), ptr(dw), ctypes.byref(d), ptr(ws), n,
+                                         stream_ptr(x.device))
+    check(rc, "sqr_conv2d_bwd_weight")
+    return dw
+
+
+def compute_dtype(x):
+    if x.dtype == torch.bfloat16:
+        return torch.bfloat16
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+        return torch.bfloat16
+    return torch.float32
+
+
+class Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride, pad, dt):
+        N, C, H, W = x.shape
+        K, _, R, S = weight.shape
+        xin = x.to(dt).contiguous(memory_format=_CL)
+        d = _desc(N, C, H, W, K, R, S, stride, pad, dt)
+        need_dx = ctx.needs_input_grad[0]
+        krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
+        y = conv2d_fwd(xin, krsc, d)
+        if bias is not None:
+            y = y + bias.to(dt).view(1, K, 1, 1)
+        ctx.d = d
+        ctx.x_dtype = x.dtype
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(xin if ctx.needs_input_grad[1] else None, crsk)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xin, crsk = ctx.saved_tensors
+        d = ctx.d
+        dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+        g = gy.to(dt).contiguous(memory_format=_CL)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if crsk is None:
+                raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
+            dx = conv2d_bwd_data(g, crsk, d).to(ctx.x_dtype)
+        if ctx.needs_input_grad[1]:
+            dw = conv2d_bwd_weight(xin, g, d)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g.float().sum(dim=(0, 2, 3))
+        return dx, dw, db, None, None, None
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0):
+    if not x.is_cuda:
+        raise ValueError("sqr conv2d runs on MI355X; got a %s tensor" % x.device)
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x))
+
+
+class Conv2d(nn.Conv2d):
+    """Drop-in nn.Conv2d (same parameters/state-dict) running libsqr's implicit-GEMM kernels.
+    Supports square kernels, symmetric padding, dilation 1, groups 1, zero padding."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if (self.groups != 1 or self.dilation != (1, 1) or self.padding_mode != "zeros"
+                or self.stride[0] != self.stride[1] or self.padding[0] != self.padding[1]
+                or isinstance(self.padding, str)):
+            raise ValueError("sqr Conv2d supports groups=1, dilation=1, symmetric stride/padding only")
+
+    def forward(self, x):
+        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0])

@@ -1,0 +1,92 @@
+"""ResNet-18 backbone with torchvision-identical module names / state-dict keys, built on the
+HIP implicit-GEMM convs (sqr.conv.Conv2d).
+
+The reference takes it from torchvision (torch/models.py:4,181: ``models.resnet18(pretrained)``),
+which is neither vendored nor installed; this restatement follows torchvision's resnet18:
+BasicBlock x [2,2,2,2], conv bias=False, BatchNorm2d(eps=1e-5, momentum=0.1), 7x7/2 stem + 3x3/2
+max-pool, adaptive average pool, kaiming_normal_(fan_out, relu) conv init, BN weight 1 / bias 0.
+"""
+import os
+import warnings
+
+import torch
+import torch.nn as nn
+
+from .conv import Conv2d
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        out = out + identity
+        return self.relu(out)
+
+
+class ResNet18(nn.Module):
+    def __init__(self, in_channels=3, num_classes=1000):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = Conv2d(in_channels, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, 2)
+        self.layer2 = self._make_layer(128, 2, stride=2)
+        self.layer3 = self._make_layer(256, 2, stride=2)
+        self.layer4 = self._make_layer(512, 2, stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _make_layer(self, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes:
+            downsample = nn.Sequential(Conv2d(self.inplanes, planes, 1, stride, 0, bias=False),
+                                       nn.BatchNorm2d(planes))
+        layers = [BasicBlock(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes
+        for _ in range(1, blocks):
+            layers.append(BasicBlock(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(self.avgpool(x), 1)
+        return self.fc(x)
+
+
+def resnet18(pretrained=False):
+    """torchvision.models.resnet18 equivalent.  ImageNet weights cannot be downloaded here: with
+    pretrained=True they are loaded from $SQR_RESNET18_WEIGHTS (a torchvision state dict) if set,
+    otherwise the model keeps its random init and a warning is issued."""
+    net = ResNet18()
+    if pretrained:
+        path = os.environ.get("SQR_RESNET18_WEIGHTS")
+        if path and os.path.exists(path):
+            net.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+        else:
+            warnings.warn("resnet18(pretrained=True): ImageNet weights unavailable offline "
+                          "(set SQR_RESNET18_WEIGHTS); using random init", stacklevel=2)
+    return net

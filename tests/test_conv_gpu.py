@@ -1,0 +1,116 @@
+"""HIP implicit-GEMM conv2d (libsqr) vs torch.nn.functional.conv2d in float64 on the CPU.
+
+Floating-point kernel -> the reference is a plain PyTorch conv of the same op (float64, CPU).
+Tolerances, relative to max|ref| of each output:
+  f32 (exact-f32 MFMA, the parity mode): 1e-5 (sums of up to 4608 products, f32 accumulate;
+      measured <= 2.7e-6)
+  bf16 inputs (f32 accumulate): y/dx rounded to bf16 -> 8e-3; dw stays f32 -> 2e-4
+  (the bf16 reference is computed from the same bf16-rounded operands).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+# (N, C, H, K, R, stride, pad) — every conv of ResNetSQ at 256x256 input + GenericNetSQ
+# shapes + odd edge cases
+RESNET = [
+    (2, 1, 256, 64, 7, 2, 3),      # conv1 (im2col path)
+    (2, 64, 64, 64, 3, 1, 1),      # layer1.*
+    (2, 64, 64, 128, 3, 2, 1),     # layer2.0.conv1
+    (2, 64, 64, 128, 1, 2, 0),     # layer2.0.downsample
+    (2, 128, 32, 128, 3, 1, 1),    # layer2.*
+    (2, 128, 32, 256, 3, 2, 1),    # layer3.0.conv1
+    (2, 128, 32, 256, 1, 2, 0),    # layer3.0.downsample
+    (2, 256, 16, 256, 3, 1, 1),    # layer3.*
+    (2, 256, 16, 512, 3, 2, 1),    # layer4.0.conv1
+    (2, 256, 16, 512, 1, 2, 0),    # layer4.0.downsample
+    (2, 512, 8, 512, 3, 1, 1),     # layer4.*
+]
+EXTRA = [
+    (3, 32, 128, 32, 3, 1, 1),     # GenericNetSQ 32-channel convs (multi-tap k tiles)
+    (3, 32, 128, 64, 3, 2, 1),
+    (1, 8, 13, 16, 3, 1, 1),       # odd spatial size, tiny channels
+    (3, 16, 9, 8, 5, 2, 2),
+    (2, 3, 31, 64, 7, 2, 3),       # C=3 im2col
+    (1, 64, 7, 128, 1, 1, 0),
+]
+
+
+def _ref(x, w, stride, pad, gy):
+    xd = x.detach().double().cpu().requires_grad_(True)
+    wd = w.detach().double().cpu().requires_grad_(True)
+    y = F.conv2d(xd, wd, stride=stride, padding=pad)
+    y.backward(gy.detach().double().cpu())
+    return y.detach(), xd.grad, wd.grad
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("shape", RESNET + EXTRA, ids=lambda s: "N%dC%dH%dK%dR%ds%dp%d" % s)
+def test_conv_fwd_bwd(shape, dtype):
+    from sqr import conv as sc
+    N, C, H, K, R, st, pad = shape
+    g = torch.Generator().manual_seed(N * 1000 + C * 10 + K)
+    x = torch.randn(N, C, H, H, generator=g)
+    w = torch.randn(K, C, R, R, generator=g) / (C * R * R) ** 0.5
+    if dtype == torch.bfloat16:
+        x = x.bfloat16().float()
+        w_used = w.bfloat16().float()
+    else:
+        w_used = w
+    Ho = (H + 2 * pad - R) // st + 1
+    gy = torch.randn(N, K, Ho, Ho, generator=g)
+    if dtype == torch.bfloat16:
+        gy = gy.bfloat16().float()
+    yr, dxr, dwr = _ref(x, w_used, st, pad, gy)
+
+    xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(C >= 8)
+    wg = w.to(DEV).requires_grad_(True)
+    y = sc.conv2d(xg, wg, None, st, pad)
+    assert y.dtype == dtype and y.shape == (N, K, Ho, Ho)
+    y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
+    torch.cuda.synchronize()
+    tol_y = 1e-5 if dtype == torch.float32 else 8e-3
+    tol_w = 1e-5 if dtype == torch.float32 else 2e-4
+    assert _rel(y, yr) <= tol_y
+    assert wg.grad.dtype == torch.float32
+    assert _rel(wg.grad, dwr) <= tol_w
+    if C >= 8:
+        assert _rel(xg.grad, dxr) <= tol_y
+
+
+def test_conv_module_matches_nn_conv2d_state_dict():
+    from sqr.conv import Conv2d
+    a = torch.nn.Conv2d(64, 128, 3, 2, 1, bias=True)
+    b = Conv2d(64, 128, 3, 2, 1, bias=True)
+    b.load_state_dict(a.state_dict())
+    assert list(a.state_dict()) == list(b.state_dict())
+    x = torch.randn(2, 64, 20, 20)
+    yr = a(x)
+    b = b.to(DEV)
+    y = b(x.to(DEV).contiguous(memory_format=torch.channels_last))
+    assert _rel(y, yr) <= 2e-6
+
+
+def test_conv_deterministic():
+    from sqr import conv as sc
+    x = torch.randn(4, 64, 32, 32, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    w = torch.randn(64, 64, 3, 3, device=DEV, requires_grad=True)
+    outs = []
+    for _ in range(2):
+        x.grad = None
+        w.grad = None
+        y = sc.conv2d(x, w, None, 1, 1)
+        y.float().square().sum().backward()
+        outs.append((y.clone(), x.grad.clone(), w.grad.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

@@ -65,3 +65,30 @@ def test_kat_example_images_small_loss():
     c = [c for c in cases("implicit_loss.npz") if str(c["name"]) == "kat10_R64"][0]
     _, _, per, _ = O.implicit_loss(c["true"], c["pred"], 64, 1.5, 260, need_grad=False)
     assert per.max() < 0.012
+
+
+@pytest.mark.parametrize("name", ["rand_R16_t1_s100", "clamp_edges_R32", "rand_R48"])
+def test_torch_restatement_matches_reference(name):
+    # oracle/ref_torch.py (the CPU baseline's loss) against the same golden vectors
+    import torch
+    import ref_torch
+    c = [c for c in cases("implicit_loss.npz") if str(c["name"]) == name][0]
+    crit = ref_torch.ImplicitLossRef(int(c["R"]), float(c["tau"]), float(c["s"]))
+    p = torch.tensor(c["pred"], requires_grad=True)
+    loss = crit(torch.tensor(c["true"]), p)
+    loss.backward()
+    assert loss.dtype == torch.float64
+    assert abs(loss.item() - float(c["loss"])) <= 1e-12 * abs(float(c["loss"]))
+    g = c["grad"]
+    assert np.abs(p.grad.numpy() - g).max() <= 2e-7 * np.abs(g).max()
+
+
+def test_torch_restatement_explicit_matches_reference():
+    import torch
+    import ref_torch
+    c = cases("explicit_loss.npz")[0]
+    p = torch.tensor(c["pred"], requires_grad=True)
+    loss = ref_torch.ExplicitLossRef(int(c["R"]))(torch.tensor(c["true"]), p)
+    loss.backward()
+    assert abs(loss.item() - float(c["loss"])) <= 1e-12 * abs(float(c["loss"]))
+    assert np.abs(p.grad.numpy() - c["grad"]).max() <= 2e-7 * np.abs(c["grad"]).max()
