@@ -22,6 +22,9 @@
  *                              torch.nn.Conv2d as used by torchvision resnet18 inside ResNetSQ
  *                              (torch/models.py:181-184) and by GenericNetSQ (torch/models.py:134-152)
  *                              — forward and the two autograd backward products.
+ *   sqr_bn_fwd / sqr_bn_bwd    torch.nn.BatchNorm2d (+ residual add + ReLU) of torchvision resnet18's
+ *                              BasicBlock (ResNetSQ encoder, torch/models.py:181), training and eval.
+ *   sqr_stem_fwd / _bwd        resnet18 stem bn1 -> relu -> maxpool(3,2,1) (torch/models.py:181).
  */
 #ifndef SQR_H
 #define SQR_H
@@ -94,19 +97,55 @@ typedef struct sqr_conv_desc {
 int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo);
 size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which /*0 fwd,1 dgrad,2 wgrad*/);
 
-/* w_kcrs f32 [K,C,R,S] -> w_krsc [K,R,S,Cp] and (optionally) w_crsk [C,R,S,K] in d->dtype.
- * Cp = C rounded up to 8 (zero-padded) so the channel dim is 16-byte vectorisable. */
+/* w_kcrs f32 [K,C,R,S] -> w_krsc [K,R,S,C] and (optionally) w_crsk [C,R,S,K] in d->dtype.
+ * For C<8 convs w_krsc is the im2col weight [K][Kp], Kp = next pow2 >= max(64, R*S*C). */
 int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* d, void* w_krsc, void* w_crsk,
                            void* stream);
-/* x [N,H,W,Cp] (Cp = C rounded up to 8), y [N,Ho,Wo,K] */
+/* x [N,H,W,C], y [N,Ho,Wo,K].  C must be a power of two >= 8, or < 8 (then the conv runs as
+ * im2col into the workspace + a 1x1 GEMM; the im2col matrix stays in the workspace). */
 int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, void* workspace,
                    size_t workspace_bytes, void* stream);
 /* dy [N,Ho,Wo,K], w_crsk [C,R,S,K] -> dx [N,H,W,C] */
 int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
                         void* workspace, size_t workspace_bytes, void* stream);
-/* x [N,H,W,Cp], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
+/* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
 int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* C<8 (im2col) convs only: the same from the im2col matrix the forward left at the start of its
+ * workspace (sqr_conv2d_workspace_bytes(d,0) bytes), skipping the re-gather; this call's own
+ * workspace needs sqr_conv2d_workspace_bytes(d,2) - sqr_conv2d_workspace_bytes(d,0) bytes. */
+int sqr_conv2d_bwd_weight_col(const void* col, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- batch norm (NHWC, fused) */
+
+/* x [M][C] (M = N*H*W pixels, NHWC), C a multiple of 8 with C/8 dividing 256; gamma/beta/stats f32.
+ * training != 0: batch statistics; save_mean/save_invstd [C] are written and running_mean/var
+ *   (nullable) are updated as nn.BatchNorm2d does (momentum, unbiased running variance);
+ * training == 0: normalises with running_mean/var.
+ * y = relu?(gamma*(x-mean)*invstd + beta [+ residual]); residual nullable. */
+size_t sqr_bn_workspace_bytes(long long M, int C);
+int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const float* gamma, const float* beta,
+               float* running_mean, float* running_var, float momentum, float eps, int training,
+               const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
+               void* workspace, size_t workspace_bytes, void* stream);
+/* backward of sqr_bn_fwd (training statistics): g = dy * [y > 0] (y = the forward output, NULL when
+ * the forward had no ReLU); dx, dgamma = sum g*xhat, dbeta = sum g; dres (nullable) = g. */
+int sqr_bn_bwd(const void* dy, const void* y, const void* x, long long M, int C, int dtype, const float* gamma,
+               const float* save_mean, const float* save_invstd, void* dx, void* dres, float* dgamma,
+               float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
+
+/* resnet stem: y = maxpool3x3/s2/p1(relu(bn(x))), x [N][H][W][C] NHWC; argmax [N][Ho][Wo][C] uint8
+ * = window tap (dh*3+dw) of the first maximum (torch's tie rule), written when training. */
+size_t sqr_stem_workspace_bytes(int N, int H, int W, int C);
+int sqr_stem_fwd(const void* x, int N, int H, int W, int C, int dtype, const float* gamma, const float* beta,
+                 float* running_mean, float* running_var, float momentum, float eps, int training, void* y,
+                 uint8_t* argmax, float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
+                 void* stream);
+/* dpool/ypool [N][Ho][Wo][C] (gradient and value of the pooled output), x = conv1 output. */
+int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t* argmax, const void* x, int N, int H, int W,
+                 int C, int dtype, const float* gamma, const float* save_mean, const float* save_invstd, void* dx,
+                 float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

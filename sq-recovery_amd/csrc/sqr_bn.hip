@@ -1,0 +1,692 @@
+// Fused NHWC BatchNorm (+ residual add) (+ ReLU) and the fused stem BN+ReLU+MaxPool(3,2,1) of
+// ResNetSQ's resnet18 backbone (torch/models.py:181; torchvision BasicBlock: conv-bn-relu,
+// conv-bn, +identity, relu), forward (training batch statistics / eval running statistics) and
+// backward.  These are the memory-bound glue between the implicit-GEMM convs.
+//
+// Layout: activations [M pixels][C] (NHWC), bf16 or f32; BN parameters/statistics f32.
+// Per-channel reductions are two-stage and deterministic: blocks accumulate float64 partial sums
+// over fixed pixel ranges (16-B vector loads, 8 channels per thread), a finalize kernel adds the
+// per-block partials in block order.  Elementwise passes are one read + one write per tensor.
+//   forward : stats(x) -> finalize(mean, invstd, running stats, scale/shift) -> y = act(x*scale+shift [+res])
+//   backward: g = dy * [y>0]; reduce(sum g, sum g*(x-mean)) -> finalize(dgamma, dbeta, k1,k2,k3)
+//             -> dx = k1*g + k3*x + k2  (and dres = g for the residual branch)
+#include <stdint.h>
+#include "sqr_common.h"
+
+namespace sqr {
+namespace bn {
+
+typedef __bf16 bf16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 8 consecutive channels as floats
+template <typename T> struct V8;
+template <> struct V8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float* v) {
+    const u32x4 u = *(const u32x4*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* v) {
+    typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+    *(bf16x8*)p = o;
+  }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float* v) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[4 + i] = b[i];
+    }
+  }
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+};
+
+__device__ __forceinline__ void load8f(const float* p, float* v) { V8<float>::load(p, v); }
+
+// block geometry for the reductions: V = C/8 channel vectors per pixel, rows = 256 / V
+// partial layout: part[blk][2][C] doubles (sum a, sum b).  4 pixels per iteration per thread so
+// that 4 independent 16-B loads are in flight (the loop is otherwise latency-bound).
+template <typename T, int MODE>
+// MODE 0: a = x, b = x^2                                  (forward statistics)
+// MODE 1: g = dy*[y>0 if y]; a = g, b = g*(x - mean)      (backward)
+__global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                     const T* __restrict__ y, const float* __restrict__ mean,
+                                                     int M, int C, int chunk, double* __restrict__ part) {
+  extern __shared__ double red[];  // [rows][V][16]
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x;
+  const int row = tid / V, v = tid - row * V;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.0;
+  float mu[8];
+  if (MODE == 1) load8f(mean + v * 8, mu);
+  const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
+  constexpr int U = 4;
+  for (int pb = p0 + row; pb < p1; pb += U * rows) {
+    float xv[U][8], g[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = pb + u * rows;
+      if (p < p1) {
+        const size_t off = (size_t)p * C + v * 8;
+        V8<T>::load(x + off, xv[u]);
+        if (MODE == 1) {
+          V8<T>::load(dy + off, g[u]);
+          if (y) {
+            float yv[8];
+            V8<T>::load(y + off, yv);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) g[u][i] = yv[i] > 0.f ? g[u][i] : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[u][i] = g[u][i] = 0.f;
+        if (MODE == 1) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) xv[u][i] = mu[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (MODE == 0) {
+          sa[i] += (double)xv[u][i];
+          sb[i] += (double)xv[u][i] * (double)xv[u][i];
+        } else {
+          sa[i] += (double)g[u][i];
+          sb[i] += (double)g[u][i] * (double)(xv[u][i] - mu[i]);
+        }
+      }
+    }
+  }
+  double* dst = red + ((size_t)row * V + v) * 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dst[i] = sa[i];
+    dst[8 + i] = sb[i];
+  }
+  __syncthreads();
+  if (row == 0) {
+    for (int r = 1; r < rows; ++r) {
+      const double* src = red + ((size_t)r * V + v) * 16;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sa[i] += src[i];
+        sb[i] += src[8 + i];
+      }
+    }
+    double* out = part + (size_t)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      out[v * 8 + i] = sa[i];
+      out[C + v * 8 + i] = sb[i];
+    }
+  }
+}
+
+// sum the per-block partials of 16 channels with 16 lanes each (lane j: blocks j, j+16, ...), then
+// add the 16 lane sums in lane order (deterministic).  Results land in s[2] of lane 0.
+__device__ __forceinline__ bool sum_partials(const double* __restrict__ part, int nblk, int C, double* s) {
+  __shared__ double red2[16][16][2];
+  const int cl = threadIdx.x & 15, j = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int k = j; k < nblk; k += 16) {
+      a += part[(size_t)k * 2 * C + c];
+      b += part[(size_t)k * 2 * C + C + c];
+    }
+  }
+  red2[j][cl][0] = a;
+  red2[j][cl][1] = b;
+  __syncthreads();
+  if (j != 0 || c >= C) return false;
+  for (int k = 1; k < 16; ++k) {
+    a += red2[k][cl][0];
+    b += red2[k][cl][1];
+  }
+  s[0] = a;
+  s[1] = b;
+  return true;
+}
+
+// forward finalize: coef[0][c] = scale, coef[1][c] = shift; save_mean/save_invstd; running stats
+__global__ void fwd_finalize_kernel(const double* __restrict__ part, int nblk, int M, int C,
+                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                    float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
+                                    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                    float* __restrict__ coef) {
+  double acc[2];
+  if (!sum_partials(part, nblk, C, acc)) return;
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const double s = acc[0], ss = acc[1];
+  const double mean = s / M;
+  double var = ss / M - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const double invstd = 1.0 / sqrt(var + (double)eps);
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float scale = (float)(g * invstd);
+  coef[c] = scale;
+  coef[C + c] = (float)(bt - mean * g * invstd);
+  save_mean[c] = (float)mean;
+  save_invstd[c] = (float)invstd;
+  if (rmean) {
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+}
+
+__global__ void infer_coef_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                  const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
+                                  float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double invstd = 1.0 / sqrt((double)rvar[c] + (double)eps);
+  const double g = gamma ? gamma[c] : 1.0, bt = beta ? beta[c] : 0.0;
+  coef[c] = (float)(g * invstd);
+  coef[C + c] = (float)(bt - rmean[c] * g * invstd);
+}
+
+// y = act(x*scale + shift [+ res])
+template <typename T>
+__global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                    const float* __restrict__ coef, int C, int nvec, int relu,
+                                                    T* __restrict__ y) {
+  const int lv = __builtin_ctz(C >> 3);
+  {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    const int v = i & ((1 << lv) - 1);
+    float xv[8], sc[8], sh[8];
+    V8<T>::load(x + i * 8, xv);
+    load8f(coef + v * 8, sc);
+    load8f(coef + C + v * 8, sh);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(xv[k], sc[k], sh[k]);
+    if (res) {
+      float rv[8];
+      V8<T>::load(res + i * 8, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
+    }
+    V8<T>::store(y + i * 8, o);
+  }
+}
+
+// backward finalize: dgamma, dbeta and dx = k1*g + k3*x + k2 coefficients (coef[0..2][C])
+__global__ void bwd_finalize_kernel(const double* __restrict__ part, int nblk, int M, int C,
+                                    const float* __restrict__ gamma, const float* __restrict__ mean,
+                                    const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, float* __restrict__ coef) {
+  double acc[2];
+  if (!sum_partials(part, nblk, C, acc)) return;
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  const double sg = acc[0], sgx = acc[1];
+  const double is = invstd[c], mu = mean[c];
+  const double dgam = sgx * is;  // sum g * xhat
+  if (dgamma) dgamma[c] = (float)dgam;
+  if (dbeta) dbeta[c] = (float)sg;
+  const double a = (gamma ? gamma[c] : 1.0) * is;
+  const double k3 = -a * is * dgam / M;
+  coef[c] = (float)a;
+  coef[2 * C + c] = (float)k3;
+  coef[C + c] = (float)(-a * sg / M - k3 * mu);
+}
+
+// dx = k1*g + k3*x + k2 with g = dy*[y>0]; optionally dres = g
+template <typename T>
+__global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                        const T* __restrict__ x, const float* __restrict__ coef,
+                                                        int C, int nvec, T* __restrict__ dx,
+                                                        T* __restrict__ dres) {
+  const int lv = __builtin_ctz(C >> 3);
+  {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    const int v = i & ((1 << lv) - 1);
+    float g[8], xv[8], k1[8], k2[8], k3[8];
+    V8<T>::load(dy + i * 8, g);
+    if (y) {
+      float yv[8];
+      V8<T>::load(y + i * 8, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    V8<T>::load(x + i * 8, xv);
+    load8f(coef + v * 8, k1);
+    load8f(coef + C + v * 8, k2);
+    load8f(coef + 2 * C + v * 8, k3);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k3[k], xv[k], k2[k]));
+    V8<T>::store(dx + i * 8, o);
+    if (dres) V8<T>::store(dres + i * 8, g);
+  }
+}
+
+// ---------------------------------------------------------------- stem: BN + ReLU + MaxPool(3,2,1)
+// y[n,oh,ow,c] = max over the 3x3 window of relu(x*scale+shift); arg = window tap of the first max
+// (strict >, row-major scan: torch's max_pool2d tie rule)
+template <typename T>
+__global__ void __launch_bounds__(256) bnrelu_maxpool_fwd_kernel(const T* __restrict__ x,
+                                                                 const float* __restrict__ coef, int N, int H, int W,
+                                                                 int C, int Ho, int Wo, FastDiv fd_wo, FastDiv fd_ho,
+                                                                 T* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int lv = __builtin_ctz(C >> 3);
+  const int nvec = N * Ho * Wo << lv;
+  {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    const int v = i & ((1 << lv) - 1);
+    const int pix = i >> lv;
+    const int q = (int)fdiv((uint32_t)pix, fd_wo);
+    const int ow = pix - q * Wo;
+    const int n = (int)fdiv((uint32_t)q, fd_ho);
+    const int oh = q - n * Ho;
+    float sc[8], sh[8], best[8];
+    uint8_t bi[8];
+    load8f(coef + v * 8, sc);
+    load8f(coef + C + v * 8, sh);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      best[k] = -INFINITY;
+      bi[k] = 0;
+    }
+    for (int dh = 0; dh < 3; ++dh) {
+      const int h = oh * 2 - 1 + dh;
+      if (h < 0 || h >= H) continue;
+      for (int dw = 0; dw < 3; ++dw) {
+        const int w = ow * 2 - 1 + dw;
+        if (w < 0 || w >= W) continue;
+        float xv[8];
+        V8<T>::load(x + (((size_t)n * H + h) * W + w) * C + v * 8, xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          // relu output rounded to the activation dtype, as the unfused path stores it
+          float t = fmaxf(fmaf(xv[k], sc[k], sh[k]), 0.f);
+          if (sizeof(T) == 2) t = (float)(bf16)t;
+          if (t > best[k]) {
+            best[k] = t;
+            bi[k] = (uint8_t)(dh * 3 + dw);
+          }
+        }
+      }
+    }
+    V8<T>::store(y + i * 8, best);
+    if (arg) {
+      uint64_t packed = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) packed |= (uint64_t)bi[k] << (8 * k);
+      *(uint64_t*)(arg + i * 8) = packed;
+    }
+  }
+}
+
+// gradient at a full-resolution pixel: sum of dpool over the (<=4) windows whose argmax is this
+// pixel and whose pooled (post-ReLU) value is > 0 — exactly maxpool-backward then ReLU-backward
+// of the unfused graph (the pooled value IS the ReLU output at the argmax pixel).
+template <typename T>
+__device__ __forceinline__ void stem_grad(const T* __restrict__ dpool, const T* __restrict__ ypool,
+                                          const uint8_t* __restrict__ arg, int n, int h, int w, int v, int C,
+                                          int Ho, int Wo, float* g) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) g[k] = 0.f;
+  const int oh0 = h >> 1, oh1 = min(Ho - 1, (h + 1) >> 1);
+  const int ow0 = w >> 1, ow1 = min(Wo - 1, (w + 1) >> 1);
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int dh = h - (oh * 2 - 1);
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int dw = w - (ow * 2 - 1);
+      const uint64_t tap = (uint64_t)(dh * 3 + dw);
+      const size_t o = (((size_t)n * Ho + oh) * Wo + ow) * C + v * 8;
+      const uint64_t a = *(const uint64_t*)(arg + o);
+      float dp[8], yp[8];
+      V8<T>::load(dpool + o, dp);
+      V8<T>::load(ypool + o, yp);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (((a >> (8 * k)) & 0xff) == tap && yp[k] > 0.f) g[k] += dp[k];
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) stem_bwd_reduce_kernel(const T* __restrict__ dpool,
+                                                              const T* __restrict__ ypool,
+                                                              const uint8_t* __restrict__ arg,
+                                                              const T* __restrict__ x, const float* __restrict__ mean,
+                                                              int N, int H, int W, int C, int Ho, int Wo, int chunk,
+                                                              FastDiv fd_w, FastDiv fd_h, double* __restrict__ part) {
+  extern __shared__ double red[];
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x;
+  const int row = tid / V, v = tid - row * V;
+  const int M = N * H * W;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.0;
+  float mu[8];
+  load8f(mean + v * 8, mu);
+  const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
+  if (row < rows) {
+    for (int p = p0 + row; p < p1; p += rows) {
+      const int q = (int)fdiv((uint32_t)p, fd_w), w = p - q * W;
+      const int n = (int)fdiv((uint32_t)q, fd_h), h = q - n * H;
+      float g[8], xv[8];
+      stem_grad<T>(dpool, ypool, arg, n, h, w, v, C, Ho, Wo, g);
+      V8<T>::load(x + (size_t)p * C + v * 8, xv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sa[i] += (double)g[i];
+        sb[i] += (double)g[i] * (double)(xv[i] - mu[i]);
+      }
+    }
+    double* dst = red + ((size_t)row * V + v) * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      dst[i] = sa[i];
+      dst[8 + i] = sb[i];
+    }
+  }
+  __syncthreads();
+  if (row == 0) {
+    for (int r = 1; r < rows; ++r) {
+      const double* src = red + ((size_t)r * V + v) * 16;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sa[i] += src[i];
+        sb[i] += src[8 + i];
+      }
+    }
+    double* out = part + (size_t)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      out[v * 8 + i] = sa[i];
+      out[C + v * 8 + i] = sb[i];
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) stem_bwd_apply_kernel(const T* __restrict__ dpool,
+                                                             const T* __restrict__ ypool,
+                                                             const uint8_t* __restrict__ arg,
+                                                             const T* __restrict__ x, const float* __restrict__ bcoef,
+                                                             int N, int H, int W, int C, int Ho, int Wo, FastDiv fd_w,
+                                                             FastDiv fd_h, T* __restrict__ dx) {
+  const int lv = __builtin_ctz(C >> 3);
+  const int nvec = N * H * W << lv;
+  {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nvec) return;
+    const int v = i & ((1 << lv) - 1);
+    const int p = i >> lv;
+    const int q = (int)fdiv((uint32_t)p, fd_w), w = p - q * W;
+    const int n = (int)fdiv((uint32_t)q, fd_h), h = q - n * H;
+    float g[8], xv[8], k1[8], k2[8], k3[8];
+    stem_grad<T>(dpool, ypool, arg, n, h, w, v, C, Ho, Wo, g);
+    V8<T>::load(x + i * 8, xv);
+    load8f(bcoef + v * 8, k1);
+    load8f(bcoef + C + v * 8, k2);
+    load8f(bcoef + 2 * C + v * 8, k3);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k3[k], xv[k], k2[k]));
+    V8<T>::store(dx + i * 8, o);
+  }
+}
+
+}  // namespace bn
+}  // namespace sqr
+
+using namespace sqr;
+using namespace sqr::bn;
+
+// ============================================================================ host side
+namespace {
+
+struct RedPlan {
+  int nblk, chunk, rows;
+  size_t lds;
+};
+
+RedPlan red_plan(int M, int C) {
+  RedPlan p;
+  const int V = C / 8;
+  p.rows = 256 / V;
+  int chunk = (M + 511) / 512;  // ~2 blocks per CU
+  chunk = chunk < p.rows * 4 ? p.rows * 4 : chunk;
+  chunk = ((chunk + p.rows - 1) / p.rows) * p.rows;
+  p.chunk = chunk;
+  p.nblk = (M + chunk - 1) / chunk;
+  p.lds = (size_t)p.rows * V * 16 * sizeof(double);
+  return p;
+}
+
+size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int check_mc(long long M, int C, int dtype) {
+  SQR_CHECK_ARG(M >= 1 && M < (1ll << 31), "bn: bad pixel count %lld", M);
+  SQR_CHECK_ARG(C >= 8 && C <= 2048 && C % 8 == 0 && (256 % (C / 8) == 0 || C / 8 > 256),
+                "bn: C=%d must be a multiple of 8 with C/8 dividing 256", C);
+  SQR_CHECK_ARG(C / 8 <= 256 && ((C / 8) & (C / 8 - 1)) == 0, "bn: C=%d must be 8 * a power of two <= 2048", C);
+  SQR_CHECK_ARG(M * (C / 8) < (1ll << 31), "bn: tensor too large");
+  SQR_CHECK_ARG(dtype == SQR_DTYPE_F32 || dtype == SQR_DTYPE_BF16, "bn: bad dtype");
+  return 0;
+}
+
+unsigned ew_grid(long long nvec) { return (unsigned)((nvec + 255) / 256); }
+
+}  // namespace
+
+extern "C" size_t sqr_bn_workspace_bytes(long long M, int C) {
+  if (M < 1 || C < 8) return 0;
+  const RedPlan p = red_plan((int)M, C);
+  return a256((size_t)p.nblk * 2 * C * sizeof(double)) + a256((size_t)3 * C * sizeof(float));
+}
+
+template <typename T>
+static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const float* beta, float* rmean,
+                       float* rvar, float momentum, float eps, int training, const void* res, int relu, void* y,
+                       float* save_mean, float* save_invstd, void* ws, hipStream_t st) {
+  const RedPlan p = red_plan(M, C);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  if (training) {
+    hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
+                       (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
+    SQR_HIP_LAUNCH_CHECK("bn reduce_kernel");
+    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+                       beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
+    SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel");
+  } else {
+    hipLaunchKernelGGL(infer_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rmean, rvar, eps,
+                       coef);
+    SQR_HIP_LAUNCH_CHECK("bn infer_coef_kernel");
+  }
+  const int nvec = M * (C / 8);
+  hipLaunchKernelGGL((apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)x, (const T*)res, coef, C,
+                     nvec, relu, (T*)y);
+  SQR_HIP_LAUNCH_CHECK("bn apply_kernel");
+  return 0;
+}
+
+extern "C" int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const float* gamma, const float* beta,
+                          float* running_mean, float* running_var, float momentum, float eps, int training,
+                          const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && y && workspace, "bn_fwd: null pointer");
+  SQR_CHECK_ARG(!training || (save_mean && save_invstd), "bn_fwd: training needs save_mean/save_invstd");
+  SQR_CHECK_ARG(training || (running_mean && running_var), "bn_fwd: eval needs running statistics");
+  if (workspace_bytes < sqr_bn_workspace_bytes(M, C)) {
+    set_error("bn_fwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return bn_fwd_impl<bf16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training,
+                             residual, relu, y, save_mean, save_invstd, workspace, st);
+  return bn_fwd_impl<float>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training, residual,
+                            relu, y, save_mean, save_invstd, workspace, st);
+}
+
+template <typename T>
+static int bn_bwd_impl(const void* dy, const void* y, const void* x, int M, int C, const float* gamma,
+                       const float* mean, const float* invstd, void* dx, void* dres, float* dgamma, float* dbeta,
+                       void* ws, hipStream_t st) {
+  const RedPlan p = red_plan(M, C);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  hipLaunchKernelGGL((reduce_kernel<T, 1>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)dy,
+                     (const T*)y, mean, M, C, p.chunk, part);
+  SQR_HIP_LAUNCH_CHECK("bn bwd reduce_kernel");
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+                     invstd, dgamma, dbeta, coef);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel");
+  const int nvec = M * (C / 8);
+  hipLaunchKernelGGL((bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dy, (const T*)y,
+                     (const T*)x, coef, C, nvec, (T*)dx, (T*)dres);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_apply_kernel");
+  return 0;
+}
+
+extern "C" int sqr_bn_bwd(const void* dy, const void* y, const void* x, long long M, int C, int dtype,
+                          const float* gamma, const float* save_mean, const float* save_invstd, void* dx, void* dres,
+                          float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(dy && x && dx && save_mean && save_invstd && workspace, "bn_bwd: null pointer");
+  if (workspace_bytes < sqr_bn_workspace_bytes(M, C)) {
+    set_error("bn_bwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return bn_bwd_impl<bf16>(dy, y, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, workspace,
+                             st);
+  return bn_bwd_impl<float>(dy, y, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, workspace,
+                            st);
+}
+
+// ---------------------------------------------------------------- stem
+extern "C" size_t sqr_stem_workspace_bytes(int N, int H, int W, int C) {
+  return sqr_bn_workspace_bytes((long long)N * H * W, C);
+}
+
+template <typename T>
+static int stem_fwd_impl(const void* x, int N, int H, int W, int C, const float* gamma, const float* beta,
+                         float* rmean, float* rvar, float momentum, float eps, int training, void* y, uint8_t* arg,
+                         float* save_mean, float* save_invstd, void* ws, hipStream_t st) {
+  const int M = N * H * W;
+  const RedPlan p = red_plan(M, C);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  if (training) {
+    hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
+                       (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
+    SQR_HIP_LAUNCH_CHECK("stem reduce_kernel");
+    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+                       beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
+    SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel");
+  } else {
+    hipLaunchKernelGGL(infer_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rmean, rvar, eps,
+                       coef);
+    SQR_HIP_LAUNCH_CHECK("stem infer_coef_kernel");
+  }
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  const long long nvec = (long long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL((bnrelu_maxpool_fwd_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)x, coef, N, H,
+                     W, C, Ho, Wo, make_fastdiv(Wo), make_fastdiv(Ho), (T*)y, arg);
+  SQR_HIP_LAUNCH_CHECK("bnrelu_maxpool_fwd_kernel");
+  return 0;
+}
+
+extern "C" int sqr_stem_fwd(const void* x, int N, int H, int W, int C, int dtype, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                            int training, void* y, uint8_t* argmax, float* save_mean, float* save_invstd,
+                            void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_mc((long long)N * H * W, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && y && workspace, "stem_fwd: null pointer");
+  SQR_CHECK_ARG(!training || (save_mean && save_invstd && argmax), "stem_fwd: training needs stats + argmax");
+  SQR_CHECK_ARG(training || (running_mean && running_var), "stem_fwd: eval needs running statistics");
+  if (workspace_bytes < sqr_stem_workspace_bytes(N, H, W, C)) {
+    set_error("stem_fwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return stem_fwd_impl<bf16>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, training, y,
+                               argmax, save_mean, save_invstd, workspace, st);
+  return stem_fwd_impl<float>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, training, y,
+                              argmax, save_mean, save_invstd, workspace, st);
+}
+
+template <typename T>
+static int stem_bwd_impl(const void* dpool, const void* ypool, const uint8_t* arg, const void* x, int N, int H,
+                         int W, int C, const float* gamma, const float* mean, const float* invstd, void* dx,
+                         float* dgamma, float* dbeta, void* ws, hipStream_t st) {
+  const int M = N * H * W;
+  const RedPlan p = red_plan(M, C);
+  double* part = (double*)ws;
+  float* bcoef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL((stem_bwd_reduce_kernel<T>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)dpool,
+                     (const T*)ypool, arg, (const T*)x, mean, N, H, W, C, Ho, Wo, p.chunk, make_fastdiv(W),
+                     make_fastdiv(H), part);
+  SQR_HIP_LAUNCH_CHECK("stem_bwd_reduce_kernel");
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+                     invstd, dgamma, dbeta, bcoef);
+  SQR_HIP_LAUNCH_CHECK("stem bwd_finalize_kernel");
+  const long long nvec = (long long)M * (C / 8);
+  hipLaunchKernelGGL((stem_bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dpool,
+                     (const T*)ypool, arg, (const T*)x, bcoef, N, H, W, C, Ho, Wo, make_fastdiv(W), make_fastdiv(H),
+                     (T*)dx);
+  SQR_HIP_LAUNCH_CHECK("stem_bwd_apply_kernel");
+  return 0;
+}
+
+extern "C" int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t* argmax, const void* x, int N, int H,
+                            int W, int C, int dtype, const float* gamma, const float* save_mean,
+                            const float* save_invstd, void* dx, float* dgamma, float* dbeta, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+  int rc = check_mc((long long)N * H * W, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(dpool && ypool && argmax && x && dx && save_mean && save_invstd && workspace,
+                "stem_bwd: null pointer");
+  if (workspace_bytes < sqr_stem_workspace_bytes(N, H, W, C)) {
+    set_error("stem_bwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return stem_bwd_impl<bf16>(dpool, ypool, argmax, x, N, H, W, C, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                               workspace, st);
+  return stem_bwd_impl<float>(dpool, ypool, argmax, x, N, H, W, C, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                              workspace, st);
+}

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <stdint.h>
 #include <stdio.h>
 #include "../../include/sqr.h"
 
@@ -27,6 +28,27 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery); built on the host
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+static inline int ilog2_ceil(int x) {
+  int l = 0;
+  while ((1 << l) < x) ++l;
+  return l;
+}
 
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {

@@ -38,23 +38,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-// n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery)
-struct FastDiv {
-  uint32_t d, m, s;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f;
-  f.d = d;
-  uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (__umulhi(n, f.m) + n) >> f.s;
-}
-
 // implicit im2col view of an NHWC tensor
 struct Gather {
   const void* base;
@@ -460,45 +443,89 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 }
 
 // dw_kcrs[k][c][r][s] = sum_z slab[z][k][(r*S+s)*Ci + c]   (c < C real channels)
-// im2col mode: column index = (r*S+s)*C + c directly (Ci = padded K of the col matrix)
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K, int Ng, int C, int R,
-                                    int S, int Ci, int im2col, float* __restrict__ dw) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over K*C*R*S in torch order
-  const int total = K * C * R * S;
-  if (idx >= total) return;
-  const int s = idx % S;
-  const int r = (idx / S) % R;
-  const int c = (idx / (S * R)) % C;
-  const int k = idx / (S * R * C);
-  const int col = im2col ? (r * S + s) * C + c : (r * S + s) * Ci + c;
-  float acc = 0.f;
+// im2col mode: column index = (r*S+s)*C + c directly (Ci = padded K of the col matrix).
+// Block = 16 column-quads x 16 split-lanes: lane z0 sums splits z0, z0+16, ... (16-B coalesced
+// reads), then the 16 partial sums are added in a fixed order through LDS -> deterministic.
+// The permuted writes to torch's KCRS layout are 4-B scatters (the output is small).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
+                                                           int Ng, int C, int R, int S, int Ci, int im2col,
+                                                           float* __restrict__ dw) {
+  __shared__ f32x4 part[16][17];
+  const int nq = Ng >> 2;
+  const int ql = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const int qidx = blockIdx.x * 16 + ql;  // over K * Ng/4
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const size_t stride = (size_t)K * Ng;
-  const float* src = slab + (size_t)k * Ng + col;
-  for (int z = 0; z < splits; ++z) acc += src[z * stride];
-  dw[idx] = acc;
+  if (qidx < K * nq) {
+    const int k = qidx / nq, col0 = (qidx - k * nq) * 4;
+    const float* src = slab + (size_t)k * Ng + col0;
+    for (int z = zl; z < splits; z += 16) acc += *(const f32x4*)(src + z * stride);
+  }
+  part[zl][ql] = acc;
+  __syncthreads();
+  if (zl != 0 || qidx >= K * nq) return;
+  for (int z = 1; z < 16; ++z) acc += part[z][ql];
+  const int k = qidx / nq, col0 = (qidx - k * nq) * 4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int col = col0 + e;
+    int tap, c;
+    if (im2col) {
+      if (col >= R * S * C) continue;
+      tap = col / C;
+      c = col - tap * C;
+    } else {
+      tap = col / Ci;
+      c = col - tap * Ci;
+    }
+    dw[((size_t)k * C + c) * R * S + tap] = acc[e];
+  }
 }
 
 // ============================================================================ helpers
-// im2col for small-C inputs: col[m][kk] = x[n][oh*st-p+r][ow*st-p+s][c], kk=(r*S+s)*C+c, zero pad
+// im2col for small-C inputs: col[m][kk] = x[n][oh*st-p+r][ow*st-p+s][c], kk=(r*S+s)*C+c, zero pad.
+// One thread per 8 consecutive kk of one row -> one 16-B (bf16) / 2x16-B (f32) store.
 template <typename T>
 __global__ void im2col_kernel(const T* __restrict__ x, int N, int H, int W, int C, int R, int S, int st,
                               int pad, int Ho, int Wo, int Kp, T* __restrict__ col) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t total = (size_t)N * Ho * Wo * Kp;
+  const int chunks = Kp >> 3;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // < 2^31 (checked on the host)
+  const int total = N * Ho * Wo * chunks;
   if (idx >= total) return;
-  const int kk = (int)(idx % Kp);
-  const size_t m = idx / Kp;
-  const int ow = (int)(m % Wo);
-  const int oh = (int)((m / Wo) % Ho);
-  const int n = (int)(m / ((size_t)Wo * Ho));
-  T v = (T)0.f;
-  if (kk < R * S * C) {
-    const int c = kk % C, tap = kk / C;
-    const int r = tap / S, s = tap % S;
-    const int h = oh * st - pad + r, w = ow * st - pad + s;
-    if (h >= 0 && h < H && w >= 0 && w < W) v = x[(((size_t)n * H + h) * W + w) * C + c];
+  const int m = idx / chunks, j = idx - m * chunks;
+  const int hw = Ho * Wo;
+  const int n = m / hw, rem = m - n * hw;
+  const int oh = rem / Wo, ow = rem - oh * Wo;
+  const T* __restrict__ xn = x + (size_t)n * H * W * C;
+  const int RSC = R * S * C;
+  int kk = j * 8;
+  int tap = kk / C, c = kk - tap * C;
+  int r = tap / S, s = tap - r * S;
+  T v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    T val = (T)0.f;
+    if (kk < RSC) {
+      const int h = oh * st - pad + r, w = ow * st - pad + s;
+      if (h >= 0 && h < H && w >= 0 && w < W) val = xn[(h * W + w) * C + c];
+    }
+    v[e] = val;
+    ++kk;
+    if (++c == C) {
+      c = 0;
+      if (++s == S) {
+        s = 0;
+        ++r;
+      }
+    }
   }
-  col[idx] = v;
+  T* dst = col + (size_t)m * Kp + j * 8;
+  if constexpr (sizeof(T) == 2) {
+    *(u32x4*)dst = __builtin_bit_cast(u32x4, v);
+  } else {
+    *(u32x4*)dst = *(u32x4*)&v[0];
+    *(u32x4*)(dst + 4) = *(u32x4*)&v[4];
+  }
 }
 
 // w_kcrs f32 -> w_krsc (T) [K][R][S][C] (or [K][Kp] im2col layout), w_crsk (T) [C][R][S][K]
@@ -560,6 +587,7 @@ int check_desc(const sqr_conv_desc* d, Shape* sh) {
   const long long M = (long long)d->N * sh->Ho * sh->Wo;
   const long long Min = (long long)d->N * d->H * d->W;
   SQR_CHECK_ARG(M < (1ll << 31) && Min < (1ll << 31), "conv2d: too many pixels");
+  SQR_CHECK_ARG(d->C >= 8 || M * 64 < (1ll << 31), "conv2d: too many pixels for the im2col path");
   sh->M = (int)M;
   sh->im2col = d->C < 8;
   sh->Kp = 64;  // im2col K: next power of two >= max(64, R*S*C) (the gather needs a power-of-2 row)
@@ -629,7 +657,7 @@ TNPlan plan_tn(int Kout, int Ng, int Mpix, int ES) {
   p.ntn = (Ng + p.bn - 1) / p.bn;
   const int BK = 128 / ES;
   const int tiles = p.ntm * p.ntn;
-  int splits = (1024 + tiles - 1) / tiles;  // ~4 workgroups per CU
+  int splits = (512 + tiles - 1) / tiles;  // ~2 workgroups per CU
   const int maxs = (Mpix + BK - 1) / BK;
   splits = splits < 1 ? 1 : (splits > maxs ? maxs : splits);
   int kchunk = (Mpix + splits - 1) / splits;
@@ -701,7 +729,7 @@ extern "C" int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* 
 
 template <typename T>
 static int im2col(const void* x, const sqr_conv_desc* d, const Shape& sh, void* col, hipStream_t st) {
-  const size_t total = (size_t)sh.M * sh.Kp;
+  const size_t total = (size_t)sh.M * (sh.Kp / 8);
   const unsigned blocks = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL((im2col_kernel<T>), dim3(blocks), dim3(256), 0, st, (const T*)x, d->N, d->H, d->W, d->C,
                      d->R, d->S, d->stride, d->pad, sh.Ho, sh.Wo, sh.Kp, (T*)col);
@@ -757,13 +785,15 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
   return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
 }
 
-extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
-                                     void* workspace, size_t workspace_bytes, void* stream) {
+static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, float* dw_kcrs,
+                           const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
   Shape sh;
   int rc = check_desc(d, &sh);
   if (rc) return rc;
-  SQR_CHECK_ARG(x && dy && dw_kcrs, "conv2d_bwd_weight: null pointer");
-  const size_t need = sqr_conv2d_workspace_bytes(d, 2);
+  SQR_CHECK_ARG((x || col_in) && dy && dw_kcrs, "conv2d_bwd_weight: null pointer");
+  SQR_CHECK_ARG(!col_in || sh.im2col, "conv2d_bwd_weight_col: only for C<8 (im2col) convs");
+  const size_t colb = sh.im2col ? align_up((size_t)sh.M * sh.Kp * sh.ES) : 0;
+  const size_t need = sqr_conv2d_workspace_bytes(d, 2) - (col_in ? colb : 0);
   if (!workspace || workspace_bytes < need) {
     set_error("conv2d_bwd_weight: workspace %zu < %zu", workspace_bytes, need);
     return SQR_E_WORKSPACE;
@@ -773,11 +803,15 @@ extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kc
   char* ws = (char*)workspace;
   int Ng;
   if (sh.im2col) {
-    rc = d->dtype == SQR_DTYPE_BF16 ? im2col<bf16>(x, d, sh, ws, st) : im2col<float>(x, d, sh, ws, st);
-    if (rc) return rc;
-    a.g = make_gather(ws, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 1, 1, 1, 1, d->N);
+    const void* col = col_in;
+    if (!col) {
+      rc = d->dtype == SQR_DTYPE_BF16 ? im2col<bf16>(x, d, sh, ws, st) : im2col<float>(x, d, sh, ws, st);
+      if (rc) return rc;
+      col = ws;
+      ws += colb;
+    }
+    a.g = make_gather(col, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 1, 1, 1, 1, d->N);
     Ng = sh.Kp;
-    ws += align_up((size_t)sh.M * sh.Kp * sh.ES);
   } else {
     a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, 1, 1, d->R, d->S, d->N);
     Ng = d->R * d->S * d->C;
@@ -789,9 +823,19 @@ extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kc
   const TNPlan p = plan_tn(d->K, Ng, sh.M, sh.ES);
   rc = d->dtype == SQR_DTYPE_BF16 ? launch_tn<bf16>(a, p, st) : launch_tn<float>(a, p, st);
   if (rc) return rc;
-  const int total = d->K * d->C * d->R * d->S;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, (const float*)ws, p.splits,
+  const int total = d->K * (Ng / 4);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, st, (const float*)ws, p.splits,
                      d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C, (int)sh.im2col, dw_kcrs);
   SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
   return 0;
+}
+
+extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  return bwd_weight_impl(x, nullptr, dy, dw_kcrs, d, workspace, workspace_bytes, stream);
+}
+
+extern "C" int sqr_conv2d_bwd_weight_col(const void* col, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+  return bwd_weight_impl(nullptr, col, dy, dw_kcrs, d, workspace, workspace_bytes, stream);
 }

@@ -45,6 +45,20 @@ SIGNATURES = {
                                     c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                       c_size_t, c_void_p]),
+    "sqr_conv2d_bwd_weight_col": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
+                                          c_size_t, c_void_p]),
+    "sqr_bn_workspace_bytes": (c_size_t, [ctypes.c_longlong, c_int]),
+    "sqr_bn_fwd": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_float, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_size_t, c_void_p]),
+    "sqr_bn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_stem_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "sqr_stem_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                             c_void_p]),
+    "sqr_stem_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 

@@ -1,0 +1,151 @@
+"""Fused BatchNorm(+residual)(+ReLU) and stem BN+ReLU+MaxPool on libsqr (sqr_bn_*, sqr_stem_*).
+
+Parameters and running statistics stay in the caller's nn.BatchNorm2d (state-dict keys
+unchanged); these functions only replace its forward/backward math with single-pass NHWC HIP
+kernels.  Training mode uses batch statistics and updates running_mean/var/num_batches_tracked
+exactly like nn.BatchNorm2d (momentum, unbiased running variance); eval mode uses the running
+statistics.
+"""
+import ctypes
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr
+
+_CL = torch.channels_last
+
+
+def _dt(t):
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError("sqr bn: unsupported dtype %s" % t.dtype)
+
+
+def _momentum(bn):
+    if bn.momentum is None:
+        return 1.0 / float(bn.num_batches_tracked.item())
+    return float(bn.momentum)
+
+
+def _ws_bytes(M, C):
+    return lib().sqr_bn_workspace_bytes(ctypes.c_longlong(M), C)
+
+
+class BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps):
+        x = x.contiguous(memory_format=_CL)
+        N, C, H, W = x.shape
+        M = N * H * W
+        if residual is not None:
+            residual = residual.to(x.dtype).contiguous(memory_format=_CL)
+        y = torch.empty_like(x, memory_format=_CL)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean = torch.empty(C, **f32)
+        invstd = torch.empty(C, **f32)
+        n = _ws_bytes(M, C)
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        check(lib().sqr_bn_fwd(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(bias),
+                               ptr(rmean) if rmean is not None else ctypes.c_void_p(0),
+                               ptr(rvar) if rvar is not None else ctypes.c_void_p(0),
+                               ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(residual), int(relu),
+                               ptr(y), ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_bn_fwd")
+        ctx.relu, ctx.training, ctx.eps = relu, training, eps
+        ctx.has_res = residual is not None
+        if training:
+            ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        else:
+            ctx.save_for_backward(x, y if relu else None, weight, rmean.clone(), rvar.clone())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, m, v = ctx.saved_tensors
+        dy = dy.to(x.dtype).contiguous(memory_format=_CL)
+        N, C, H, W = x.shape
+        M = N * H * W
+        if not ctx.training:  # eval-mode backward (running statistics are constants): plain torch
+            g = dy.float() * (y > 0) if y is not None else dy.float()
+            invstd = torch.rsqrt(v + ctx.eps)
+            xhat = (x.float() - m.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
+            dx = (g * (weight * invstd).view(1, C, 1, 1)).to(x.dtype)
+            dres = g.to(x.dtype) if ctx.has_res else None
+            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None
+        dx = torch.empty_like(x, memory_format=_CL)
+        dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        n = _ws_bytes(M, C)
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        check(lib().sqr_bn_bwd(ptr(dy), ptr(y), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
+                               ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
+                               stream_ptr(x.device)), "sqr_bn_bwd")
+        if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
+            dres = dy
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None
+
+
+def bn_act(x, bn, residual=None, relu=True):
+    """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics."""
+    training = bn.training or not bn.track_running_stats
+    if training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps))
+
+
+class StemFn(torch.autograd.Function):
+    """maxpool3x3/2/1(relu(bn(x))) — torchvision resnet stem after conv1."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, rmean, rvar, training, momentum, eps):
+        x = x.contiguous(memory_format=_CL)
+        N, C, H, W = x.shape
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty((N, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=_CL)
+        arg = torch.empty((N, Ho, Wo, C), dtype=torch.uint8, device=x.device) if training else None
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean = torch.empty(C, **f32)
+        invstd = torch.empty(C, **f32)
+        n = lib().sqr_stem_workspace_bytes(N, H, W, C)
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        check(lib().sqr_stem_fwd(ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(bias),
+                                 ptr(rmean) if rmean is not None else ctypes.c_void_p(0),
+                                 ptr(rvar) if rvar is not None else ctypes.c_void_p(0), ctypes.c_float(momentum),
+                                 ctypes.c_float(eps), int(training), ptr(y), ptr(arg), ptr(mean), ptr(invstd), ptr(ws),
+                                 n, stream_ptr(x.device)), "sqr_stem_fwd")
+        if not training:
+            ctx.mark_non_differentiable(y)
+        ctx.save_for_backward(x, y, arg, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, arg, weight, mean, invstd = ctx.saved_tensors
+        if arg is None:
+            raise RuntimeError("sqr stem: backward through an eval-mode stem is not supported")
+        dy = dy.to(x.dtype).contiguous(memory_format=_CL)
+        N, C, H, W = x.shape
+        dx = torch.empty_like(x, memory_format=_CL)
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        n = lib().sqr_stem_workspace_bytes(N, H, W, C)
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        check(lib().sqr_stem_bwd(ptr(dy), ptr(y), ptr(arg), ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(mean),
+                                 ptr(invstd), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n, stream_ptr(x.device)),
+              "sqr_stem_bwd")
+        return dx, dgamma, dbeta, None, None, None, None, None
+
+
+def stem(x, bn):
+    training = bn.training or not bn.track_running_stats
+    if training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
+    rm = bn.running_mean if bn.track_running_stats else None
+    rv = bn.running_var if bn.track_running_stats else None
+    return StemFn.apply(x, bn.weight, bn.bias, rm, rv, bool(training), mom, float(bn.eps))

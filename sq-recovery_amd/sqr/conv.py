@@ -82,7 +82,8 @@ def pack_weight(weight, d, need_crsk):
     return krsc, crsk
 
 
-def conv2d_fwd(x, w_krsc, d):
+def conv2d_fwd(x, w_krsc, d, return_ws=False):
+    """y = conv(x); with return_ws the workspace (holding the im2col matrix for C<8) is returned too."""
     import ctypes
     ho, wo = _out_hw(d)
     dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
@@ -91,7 +92,7 @@ def conv2d_fwd(x, w_krsc, d):
     with _Probe("fwd", d):
         rc = lib().sqr_conv2d_fwd(ptr(x), ptr(w_krsc), ptr(y), ctypes.byref(d), ptr(ws), n, stream_ptr(x.device))
     check(rc, "sqr_conv2d_fwd")
-    return y
+    return (y, ws) if return_ws else y
 
 
 def conv2d_bwd_data(gy, w_crsk, d):
@@ -106,13 +107,22 @@ def conv2d_bwd_data(gy, w_crsk, d):
     return dx
 
 
-def conv2d_bwd_weight(x, gy, d):
+def conv2d_bwd_weight(x, gy, d, col=None):
+    """dW (fp32, [K,C,R,S]); for C<8 convs pass the forward's workspace as `col` to skip im2col."""
     import ctypes
-    dw = torch.empty((d.K, d.C, d.R, d.S), dtype=torch.float32, device=x.device)
-    ws, n = _ws(d, 2, x.device)
+    dw = torch.empty((d.K, d.C, d.R, d.S), dtype=torch.float32, device=gy.device)
+    L = lib()
+    n = L.sqr_conv2d_workspace_bytes(ctypes.byref(d), 2)
+    if col is not None:
+        n -= L.sqr_conv2d_workspace_bytes(ctypes.byref(d), 0)
+    ws = torch.empty(max(n, 16), dtype=torch.uint8, device=gy.device)
     with _Probe("wgrad", d):
-        rc = lib().sqr_conv2d_bwd_weight(ptr(x), ptr(gy), ptr(dw), ctypes.byref(d), ptr(ws), n,
-                                         stream_ptr(x.device))
+        if col is not None:
+            rc = L.sqr_conv2d_bwd_weight_col(ptr(col), ptr(gy), ptr(dw), ctypes.byref(d), ptr(ws), n,
+                                             stream_ptr(gy.device))
+        else:
+            rc = L.sqr_conv2d_bwd_weight(ptr(x), ptr(gy), ptr(dw), ctypes.byref(d), ptr(ws), n,
+                                         stream_ptr(gy.device))
     check(rc, "sqr_conv2d_bwd_weight")
     return dw
 
@@ -134,18 +144,20 @@ class Conv2dFn(torch.autograd.Function):
         d = _desc(N, C, H, W, K, R, S, stride, pad, dt)
         need_dx = ctx.needs_input_grad[0]
         krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
-        y = conv2d_fwd(xin, krsc, d)
+        y, ws = conv2d_fwd(xin, krsc, d, return_ws=True)
         if bias is not None:
             y = y + bias.to(dt).view(1, K, 1, 1)
         ctx.d = d
         ctx.x_dtype = x.dtype
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(xin if ctx.needs_input_grad[1] else None, crsk)
+        need_w = ctx.needs_input_grad[1]
+        col = ws if (need_w and C < 8) else None  # im2col matrix, reused by the weight gradient
+        ctx.save_for_backward(xin if (need_w and col is None) else None, crsk, col)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        xin, crsk = ctx.saved_tensors
+        xin, crsk, col = ctx.saved_tensors
         d = ctx.d
         dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
         g = gy.to(dt).contiguous(memory_format=_CL)
@@ -155,7 +167,7 @@ class Conv2dFn(torch.autograd.Function):
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
             dx = conv2d_bwd_data(g, crsk, d).to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
-            dw = conv2d_bwd_weight(xin, g, d)
+            dw = conv2d_bwd_weight(xin, g, d, col)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
         return dx, dw, db, None, None, None

@@ -12,6 +12,7 @@ import warnings
 import torch
 import torch.nn as nn
 
+from .bn import bn_act, stem
 from .conv import Conv2d
 
 
@@ -29,13 +30,12 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        # conv -> fused [bn+relu] -> conv -> fused [bn + identity + relu]   (libsqr kernels)
+        out = bn_act(self.conv1(x), self.bn1, relu=True)
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
         if self.downsample is not None:
-            identity = self.downsample(x)
-        out = out + identity
-        return self.relu(out)
+            identity = bn_act(self.downsample[0](x), self.downsample[1], relu=False)
+        return bn_act(self.conv2(out), self.bn2, residual=identity, relu=True)
 
 
 class ResNet18(nn.Module):
@@ -71,7 +71,7 @@ class ResNet18(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = stem(self.conv1(x), self.bn1)  # fused bn1 -> relu -> maxpool
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

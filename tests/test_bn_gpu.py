@@ -1,0 +1,113 @@
+"""Fused NHWC BatchNorm(+residual)(+ReLU) and stem BN+ReLU+MaxPool (libsqr) vs torch.nn on CPU
+(float64).  Tolerances relative to max|ref|: f32 1e-5 (outputs, grads); bf16 1e-2 (bf16 storage)."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+
+
+def _bn(C, seed):
+    g = torch.Generator().manual_seed(seed)
+    bn = nn.BatchNorm2d(C)
+    bn.weight.data = torch.rand(C, generator=g) + 0.5
+    bn.bias.data = torch.randn(C, generator=g) * 0.1
+    bn.running_mean.data = torch.randn(C, generator=g) * 0.1
+    bn.running_var.data = torch.rand(C, generator=g) + 0.5
+    return bn
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("cfg", [(4, 64, 16, True, False), (2, 128, 9, True, True), (3, 512, 4, False, False),
+                                 (2, 256, 8, False, True), (1, 8, 5, True, True)],
+                         ids=lambda c: "N%dC%dH%d_relu%d_res%d" % c)
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+def test_bn_act(cfg, dtype, training):
+    from sqr.bn import bn_act
+    N, C, H, relu, res = cfg
+    g = torch.Generator().manual_seed(C + H)
+    x = (torch.randn(N, C, H, H, generator=g) * 2 + 0.5)
+    r = torch.randn(N, C, H, H, generator=g) if res else None
+    gy = torch.randn(N, C, H, H, generator=g)
+    if dtype == torch.bfloat16:
+        x, gy = x.bfloat16().float(), gy.bfloat16().float()
+        r = r.bfloat16().float() if r is not None else None
+    bn_ref = _bn(C, 1).double().train(training)
+    bn_gpu = copy.deepcopy(_bn(C, 1)).to(DEV).train(training)
+    xr = x.double().requires_grad_(True)
+    rr = r.double().requires_grad_(True) if r is not None else None
+    y_ref = bn_ref(xr)
+    if rr is not None:
+        y_ref = y_ref + rr
+    if relu:
+        y_ref = F.relu(y_ref)
+    y_ref.backward(gy.double())
+
+    xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    rg = r.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True) if r is not None else None
+    y = bn_act(xg, bn_gpu, residual=rg, relu=relu)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(y, y_ref) <= tol
+    assert _rel(xg.grad, xr.grad) <= (tol if dtype == torch.float32 else 3e-2)
+    assert _rel(bn_gpu.weight.grad, bn_ref.weight.grad) <= (tol if dtype == torch.float32 else 3e-2)
+    assert _rel(bn_gpu.bias.grad, bn_ref.bias.grad) <= (tol if dtype == torch.float32 else 3e-2)
+    if rg is not None:
+        assert _rel(rg.grad, rr.grad) <= tol
+    assert _rel(bn_gpu.running_mean, bn_ref.running_mean) <= 1e-6
+    assert _rel(bn_gpu.running_var, bn_ref.running_var) <= 1e-6
+    assert int(bn_gpu.num_batches_tracked) == int(bn_ref.num_batches_tracked)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("shape", [(2, 64, 32), (3, 64, 17), (1, 8, 6)], ids=lambda s: "N%dC%dH%d" % s)
+def test_stem_bn_relu_maxpool(shape, dtype):
+    from sqr.bn import stem
+    N, C, H = shape
+    g = torch.Generator().manual_seed(H)
+    x = torch.randn(N, C, H, H, generator=g)
+    if dtype == torch.bfloat16:
+        x = x.bfloat16().float()
+    Ho = (H - 1) // 2 + 1
+    gy = torch.randn(N, C, Ho, Ho, generator=g)
+    if dtype == torch.bfloat16:
+        gy = gy.bfloat16().float()
+    bn_ref = _bn(C, 2).double().train()
+    bn_gpu = _bn(C, 2).to(DEV).train()
+    xr = x.double().requires_grad_(True)
+    y_ref = F.max_pool2d(F.relu(bn_ref(xr)), 3, 2, 1)
+    y_ref.backward(gy.double())
+    xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = stem(xg, bn_gpu)
+    y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert y.shape == y_ref.shape
+    assert _rel(y, y_ref) <= tol
+    if dtype == torch.float32:
+        assert _rel(xg.grad, xr.grad) <= tol
+        assert _rel(bn_gpu.weight.grad, bn_ref.weight.grad) <= tol
+    else:
+        # bf16: ties / near-ties in the max can route the gradient to a different pixel; compare sums
+        assert abs(xg.grad.float().sum().item() - xr.grad.sum().item()) <= 3e-2 * xr.grad.abs().sum().item()
+    assert _rel(bn_gpu.running_mean, bn_ref.running_mean) <= 1e-6
+
+
+def test_stem_eval_matches_torch():
+    from sqr.bn import stem
+    x = torch.randn(2, 64, 20, 20)
+    bn = _bn(64, 3).eval()
+    ref = F.max_pool2d(F.relu(bn(x)), 3, 2, 1)
+    with torch.no_grad():
+        y = stem(x.to(DEV).contiguous(memory_format=torch.channels_last), bn.to(DEV))
+    assert _rel(y, ref) <= 1e-5
