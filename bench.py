@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--render", type=int, default=32, help="ImplicitLoss render size R")
     ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline steps (0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print a per-phase timing breakdown to stderr")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the whole train step in a HIP graph (1/0; default: on for 1 GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,14 +115,11 @@ def main():
         from torch.nn.parallel import DistributedDataParallel as DDP
         model = DDP(net, device_ids=[local], bucket_cap_mb=16, gradient_as_bucket_view=True,
                     broadcast_buffers=False)
-    try:
-        opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0, fused=True)
-    except Exception:
-        opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0)
+    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0, fused=True, capturable=use_graph)
     crit = classes.ImplicitLoss(R, dev, 1.5, 260)
 
-    def step():
-        opt.zero_grad(set_to_none=True)
+    def body():
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = model(images)
         pred = torch.cat([o.float() for o in out], dim=1)
@@ -128,6 +127,30 @@ def main():
         loss.backward()
         opt.step()
         return loss.detach()
+
+    def eager_step():
+        opt.zero_grad(set_to_none=True)
+        return body()
+
+    step = eager_step
+    if use_graph:
+        # whole-step HIP graph: forward + fused loss + backward + Adam replayed as one launch
+        # (the libsqr kernels are enqueued on torch's current stream, so they are captured too)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            static_loss = body()
+
+        def graph_step():
+            graph.replay()
+            return static_loss
+        step = graph_step
 
     def barrier():
         if world > 1:
@@ -139,14 +162,22 @@ def main():
     barrier()
 
     pc, ph, pr, ps = PROBE[1], PROBE[2], PROBE[3], PROBE[4]
-    sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
     loss_acc = torch.zeros((), dtype=torch.float64, device=dev)
+    if not use_graph:
+        sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss_acc += step()
     barrier()
     dt = time.perf_counter() - t0
+    if use_graph:
+        # HIP events cannot time a kernel inside a replayed graph: time the same kernel (same
+        # shapes/inputs) over a few eager steps of the same training loop right after.
+        sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
+        for _ in range(5):
+            eager_step()
+        torch.cuda.synchronize()
     events = sconv.probe_events()
     sconv.set_probe(None, 0, 0, 0, 0, 0, 0)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
@@ -189,7 +220,7 @@ def main():
                       "model": "ResNetSQ (resnet18 backbone, 11.37M params)", "global_batch": B * world,
                       "per_gpu_batch": B, "image": "256x256x1", "render_size": R,
                       "parallelism": "dp%d" % world},
-           "mean_loss": mean_loss, "roofline": roof}
+           "mean_loss": mean_loss, "hip_graph": use_graph, "roofline": roof}
 
     if rank == 0 and world == 1 and args.cpu_steps > 0:
         imgs_cpu = images.detach().cpu()

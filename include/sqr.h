@@ -97,15 +97,29 @@ typedef struct sqr_conv_desc {
 int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo);
 size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which /*0 fwd,1 dgrad,2 wgrad*/);
 
-/* w_kcrs f32 [K,C,R,S] -> w_krsc [K,R,S,C] and (optionally) w_crsk [C,R,S,K] in d->dtype.
+/* w_kcrs f32 [K,C,R,S] -> w_krsc [K,R,S,C] and (optionally) the backward-data weight w_crsk in
+ * d->dtype (C*R*S*K elements).  For stride 1 w_crsk is [C,R,S,K]; for stride st it holds the st*st
+ * output-parity classes (ph,pw) back to back, each [C][Rc][Sc][K] with the taps r = r0 + st*t,
+ * r0 = (ph + pad) % st (those are the only taps that reach an output pixel of that parity).
  * For C<8 convs w_krsc is the im2col weight [K][Kp], Kp = next pow2 >= max(64, R*S*C). */
 int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* d, void* w_krsc, void* w_crsk,
                            void* stream);
+/* Several pack_weight calls in ONE launch (njobs <= 20, stride <= 2; jobs is a host array read at call time;
+ * only desc K,C,R,S,stride,pad,dtype matter). */
+typedef struct sqr_pack_job {
+  const float* w_kcrs;
+  sqr_conv_desc desc;
+  void* w_krsc;
+  void* w_crsk; /* nullable */
+} sqr_pack_job;
+int sqr_conv2d_pack_weights(const sqr_pack_job* jobs, int njobs, void* stream);
+
 /* x [N,H,W,C], y [N,Ho,Wo,K].  C must be a power of two >= 8, or < 8 (then the conv runs as
  * im2col into the workspace + a 1x1 GEMM; the im2col matrix stays in the workspace). */
 int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, void* workspace,
                    size_t workspace_bytes, void* stream);
-/* dy [N,Ho,Wo,K], w_crsk [C,R,S,K] -> dx [N,H,W,C] */
+/* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1
+ * implicit GEMM per output-parity class (no work on structurally zero taps). */
 int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
                         void* workspace, size_t workspace_bytes, void* stream);
 /* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */

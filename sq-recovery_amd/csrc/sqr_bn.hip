@@ -141,29 +141,24 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
   }
 }
 
-// sum the per-block partials of 16 channels with 16 lanes each (lane j: blocks j, j+16, ...), then
-// add the 16 lane sums in lane order (deterministic).  Results land in s[2] of lane 0.
-__device__ __forceinline__ bool sum_partials(const double* __restrict__ part, int nblk, int C, double* s) {
-  __shared__ double red2[16][16][2];
-  const int cl = threadIdx.x & 15, j = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
+// one wave per channel: lane l sums partials l, l+64, ... then a fixed xor-tree wave reduction
+// (deterministic).  Block = 4 waves = 4 channels; returns false for lanes/channels with nothing to do.
+__device__ __forceinline__ bool sum_partials(const double* __restrict__ part, int nblk, int C, double* s, int* cout) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int k = j; k < nblk; k += 16) {
+    for (int k = lane; k < nblk; k += 64) {
       a += part[(size_t)k * 2 * C + c];
       b += part[(size_t)k * 2 * C + C + c];
     }
   }
-  red2[j][cl][0] = a;
-  red2[j][cl][1] = b;
-  __syncthreads();
-  if (j != 0 || c >= C) return false;
-  for (int k = 1; k < 16; ++k) {
-    a += red2[k][cl][0];
-    b += red2[k][cl][1];
-  }
+  a = wave_sum_d(a);
+  b = wave_sum_d(b);
+  if (lane != 0 || c >= C) return false;
   s[0] = a;
   s[1] = b;
+  *cout = c;
   return true;
 }
 
@@ -174,8 +169,8 @@ __global__ void fwd_finalize_kernel(const double* __restrict__ part, int nblk, i
                                     float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                     float* __restrict__ coef) {
   double acc[2];
-  if (!sum_partials(part, nblk, C, acc)) return;
-  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  int c;
+  if (!sum_partials(part, nblk, C, acc, &c)) return;
   const double s = acc[0], ss = acc[1];
   const double mean = s / M;
   double var = ss / M - mean * mean;
@@ -242,8 +237,8 @@ __global__ void bwd_finalize_kernel(const double* __restrict__ part, int nblk, i
                                     const float* __restrict__ invstd, float* __restrict__ dgamma,
                                     float* __restrict__ dbeta, float* __restrict__ coef) {
   double acc[2];
-  if (!sum_partials(part, nblk, C, acc)) return;
-  const int c = blockIdx.x * 16 + (threadIdx.x & 15);
+  int c;
+  if (!sum_partials(part, nblk, C, acc, &c)) return;
   const double sg = acc[0], sgx = acc[1];
   const double is = invstd[c], mu = mean[c];
   const double dgam = sgx * is;  // sum g * xhat
@@ -392,17 +387,32 @@ __global__ void __launch_bounds__(256) stem_bwd_reduce_kernel(const T* __restric
   load8f(mean + v * 8, mu);
   const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
   if (row < rows) {
-    for (int p = p0 + row; p < p1; p += rows) {
-      const int q = (int)fdiv((uint32_t)p, fd_w), w = p - q * W;
-      const int n = (int)fdiv((uint32_t)q, fd_h), h = q - n * H;
-      float g[8], xv[8];
-      stem_grad<T>(dpool, ypool, arg, n, h, w, v, C, Ho, Wo, g);
-      V8<T>::load(x + (size_t)p * C + v * 8, xv);
+    constexpr int U = 4;
+    for (int pb = p0 + row; pb < p1; pb += U * rows) {
+      float g[U][8], xv[U][8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        sa[i] += (double)g[i];
-        sb[i] += (double)g[i] * (double)(xv[i] - mu[i]);
+      for (int u = 0; u < U; ++u) {
+        const int p = pb + u * rows;
+        if (p < p1) {
+          const int q = (int)fdiv((uint32_t)p, fd_w), w = p - q * W;
+          const int n = (int)fdiv((uint32_t)q, fd_h), h = q - n * H;
+          stem_grad<T>(dpool, ypool, arg, n, h, w, v, C, Ho, Wo, g[u]);
+          V8<T>::load(x + (size_t)p * C + v * 8, xv[u]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            g[u][i] = 0.f;
+            xv[u][i] = mu[i];
+          }
+        }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          sa[i] += (double)g[u][i];
+          sb[i] += (double)g[u][i] * (double)(xv[u][i] - mu[i]);
+        }
     }
     double* dst = red + ((size_t)row * V + v) * 16;
 #pragma unroll
@@ -519,7 +529,7 @@ static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const fl
     hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
                        (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("bn reduce_kernel");
-    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel");
   } else {
@@ -565,7 +575,7 @@ static int bn_bwd_impl(const void* dy, const void* y, const void* x, int M, int 
   hipLaunchKernelGGL((reduce_kernel<T, 1>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)dy,
                      (const T*)y, mean, M, C, p.chunk, part);
   SQR_HIP_LAUNCH_CHECK("bn bwd reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel");
   const int nvec = M * (C / 8);
@@ -610,7 +620,7 @@ static int stem_fwd_impl(const void* x, int N, int H, int W, int C, const float*
     hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
                        (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("stem reduce_kernel");
-    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel");
   } else {
@@ -660,7 +670,7 @@ static int stem_bwd_impl(const void* dpool, const void* ypool, const uint8_t* ar
                      (const T*)ypool, arg, (const T*)x, mean, N, H, W, C, Ho, Wo, p.chunk, make_fastdiv(W),
                      make_fastdiv(H), part);
   SQR_HIP_LAUNCH_CHECK("stem_bwd_reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 15) / 16), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, bcoef);
   SQR_HIP_LAUNCH_CHECK("stem bwd_finalize_kernel");
   const long long nvec = (long long)M * (C / 8);

@@ -7,8 +7,9 @@
 //
 //   conv_nt_kernel  (forward, backward-data): out[m][n] = sum_k Q[m][k] * P[n][k]
 //       Q = implicit im2col of an NHWC tensor (X for fwd, dY for dgrad), k = (tap, channel),
-//           gathered on the fly (src pixel = (o*ms + off + tap*ks) / div, zero outside / not
-//           divisible — the strided dgrad is a gather with div = stride);
+//           gathered on the fly (src pixel = o*ms + off + tap*ks, zero outside); a strided
+//           dgrad runs as stride*stride parity classes, each a stride-1 gather over dY with only
+//           the taps of that class (no multiplications by structural zeros);
 //       P = packed weights, k-contiguous ([K][R][S][C] fwd, [C][R][S][K] dgrad).
 //       LDS rows are 128 B (64 bf16 / 32 f32 of k) with a 16-B-slot XOR swizzle
 //       slot ^= (row>>1)&7 that makes the ds_read_b128 fragment reads conflict-free.
@@ -43,17 +44,20 @@ struct Gather {
   const void* base;
   int Hi, Wi, Ci, log2Ci;  // source tensor [N][Hi][Wi][Ci]
   int Ho, Wo;              // pixel grid of the GEMM rows
-  int ms, off, div, ks;    // src = (o*ms + off + r*ks) / div
+  int ms, off_h, off_w, ks; // src = o*ms + off + r*ks
   int R, S;
   int M;                   // N*Ho*Wo
   FastDiv fd_hw, fd_w;     // divide by Ho*Wo, Wo
+  FastDiv fd_s;            // divide by S (tap -> r, s)
+  uint32_t bytes;          // size of the source tensor (buffer-descriptor range)
 };
 
 struct NTArgs {
   Gather g;        // Q operand  [M][Kg]
   const void* w;   // P operand  [Nout][Kg]
   int Nout, Kg;    // Kg = R*S*Ci (multiple of 8)
-  void* out;       // [M][Nout]
+  void* out;       // [M][Nout] (os == 1) or the strided pixel subset of an [N][oH][oW][Nout] tensor
+  int os, oph, opw, oH, oW;  // out pixel of row (n,i,j) = (n, i*os+oph, j*os+opw)
   int ntm, ntn;    // tile counts
 };
 
@@ -101,98 +105,119 @@ __device__ __forceinline__ f32x4 mfma(float a, float b, const f32x4& c) {
 }
 
 // ============================================================================ NT (fwd / dgrad)
-template <typename T, int BM, int BN, int WAVES_M, int WAVES_N>
+// 16-B zero source for LDS-DMA lanes whose im2col element lies in the padding
+__device__ __attribute__((aligned(64))) unsigned int g_zero16[16];
+
+// transposing LDS read (gfx950 ds_read_b64_tr_b16) as inline asm: the builtin form makes hipcc
+// wait vmcnt(0) for every in-flight LDS-DMA before it (it cannot rule out aliasing), which would
+// serialise the DMA ring.  The caller waits lgkmcnt itself (tr_wait) before using the results.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
+}
+__device__ __forceinline__ s16x4 ds_read_tr16(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+__device__ __forceinline__ void tr_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_row_block) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_row_block, 16, 0, 0);
+}
+
+// STAGES-deep LDS ring filled by global_load_lds_dwordx4 (LDS-DMA: no staging registers, no
+// ds_write).  One wave-instruction writes 1 KiB = 8 LDS rows x 8 slots; lane l lands in physical
+// slot l&7 of row l>>3, so each lane loads the LOGICAL slot (l&7) ^ swz(row) — the XOR swizzle is
+// applied on the source address (rule: linear LDS destination, inverse-swizzled source).  Loads of
+// tiles kt+1..kt+STAGES-1 stay in flight across the raw s_barrier; a counted s_waitcnt vmcnt
+// retires exactly the tile read next.
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
 __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
   using C = Cfg<T>;
   constexpr int BK = 128 / C::ES;  // k elements per LDS row (128 B)
   constexpr int ROWB = 128;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int QV = BM / 32, PV = BN / 32;  // 16-B vectors per thread per tile
+  constexpr int QV = BM / 32, PV = BN / 32;  // glds per wave per tile for Q / P
+  constexpr int PER_TILE = QV + PV;
   static_assert(WAVES_M * WAVES_N == 4, "4 waves");
-  constexpr int TILE_Q = BM * ROWB, TILE_P = BN * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_Q + TILE_P) + 64 * 8];
-  int2* taptab = (int2*)(smem + 2 * (TILE_Q + TILE_P));
+  constexpr int TILE_Q = BM * ROWB, TILE_P = BN * ROWB, STAGE = TILE_Q + TILE_P;
+  // ONE __shared__ array, no other LDS reads in the loop: an LDS read that may alias an in-flight
+  // LDS-DMA makes hipcc insert s_waitcnt vmcnt(0) in front of it (that killed the pipeline when
+  // the tap table lived in LDS) — tap -> (r, s) is computed with a multiply-high instead.
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
   const Gather& g = a.g;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_m = bid / a.ntn, tile_n = bid % a.ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  for (int t = tid; t < g.R * g.S; t += 256) {
-    const int r = t / g.S, s = t - r * g.S;
-    taptab[t] = make_int2(r * g.ks, s * g.ks);
-  }
-
-  // per-thread Q rows (fixed across the k loop)
-  const int lrow = tid >> 3, lvec = tid & 7;
-  int q_pix[QV], q_hb[QV], q_wb[QV];
+  // this lane's rows: r_i = 8*(4i + wave) + (lane>>3); its logical slot is the same for every i.
+  // Loads go through buffer descriptors: an out-of-range voffset returns zeros, so padding /
+  // out-of-tensor lanes just get voffset = kOOB and the per-row work is a few 32-bit VALU ops.
+  constexpr uint32_t kOOB = 0x80000000u;
+  const int lrow = lane >> 3;
+  const int lslot = (lane & 7) ^ ((4 * wave + (lane >> 4)) & 7);
+  int q_off[QV], q_hb[QV], q_wb[QV];
 #pragma unroll
   for (int i = 0; i < QV; ++i) {
-    const int m = m0 + lrow + 32 * i;
+    const int m = m0 + 8 * (4 * i + wave) + lrow;
     if (m < g.M) {
       const int n = (int)fdiv((uint32_t)m, g.fd_hw);
       const int rem = m - n * g.Ho * g.Wo;
       const int oh = (int)fdiv((uint32_t)rem, g.fd_w);
       const int ow = rem - oh * g.Wo;
-      q_pix[i] = n * g.Hi * g.Wi;
-      q_hb[i] = oh * g.ms + g.off;
-      q_wb[i] = ow * g.ms + g.off;
+      q_hb[i] = oh * g.ms + g.off_h;
+      q_wb[i] = ow * g.ms + g.off_w;
+      q_off[i] = ((n * g.Hi + q_hb[i]) * g.Wi + q_wb[i]) * g.Ci * C::ES;  // may be < 0 (padding)
     } else {
-      q_pix[i] = -1;
-      q_hb[i] = q_wb[i] = 0;
+      q_hb[i] = q_wb[i] = -(1 << 28);  // fails every bounds test
+      q_off[i] = 0;
     }
   }
-  const T* __restrict__ qbase = (const T*)g.base;
-  const T* __restrict__ wbase = (const T*)a.w;
+  uint32_t p_off[PV];
+#pragma unroll
+  for (int i = 0; i < PV; ++i) {
+    const int n = n0 + 8 * (4 * i + wave) + lrow;
+    p_off[i] = n < a.Nout ? (uint32_t)(n * a.Kg * C::ES) : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t qsrd = __builtin_amdgcn_make_buffer_rsrc((void*)g.base, 0, g.bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t psrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, (uint32_t)(a.Nout * a.Kg * C::ES), 0x00020000);
   const int RS = g.R * g.S;
   const int nkt = (a.Kg + BK - 1) / BK;
 
-  u32x4 qreg[QV], preg[PV];
-  auto load_tile = [&](int kt) {
-    const int k = kt * BK + lvec * C::VEC;
+  auto issue = [&](int kt, int stage) {
+    char* q = smem + stage * STAGE;
+    char* p = q + TILE_Q;
+    const int k = kt * BK + lslot * C::VEC;
     const int tap = k >> g.log2Ci;
     const int c = k & (g.Ci - 1);
-    int2 d = make_int2(0, 0);
     const bool tap_ok = tap < RS;
-    if (tap_ok) d = taptab[tap];
+    const int tr = (int)fdiv((uint32_t)tap, g.fd_s);
+    const int dh = tr * g.ks, dw = (tap - tr * g.S) * g.ks;
+    const int tapoff = ((dh * g.Wi + dw) * g.Ci + c) * C::ES;
 #pragma unroll
     for (int i = 0; i < QV; ++i) {
-      u32x4 v = {0u, 0u, 0u, 0u};
-      int h = q_hb[i] + d.x, w = q_wb[i] + d.y;
-      bool ok = tap_ok && q_pix[i] >= 0;
-      if (g.div > 1) {
-        ok = ok && h >= 0 && w >= 0 && (h % g.div) == 0 && (w % g.div) == 0;
-        h /= g.div;
-        w /= g.div;
-      }
-      ok = ok && h >= 0 && h < g.Hi && w >= 0 && w < g.Wi;
-      if (ok) v = *(const u32x4*)(qbase + ((size_t)(q_pix[i] + h * g.Wi + w) * g.Ci + c));
-      qreg[i] = v;
+      const int h = q_hb[i] + dh, w = q_wb[i] + dw;
+      const bool ok = tap_ok && (unsigned)h < (unsigned)g.Hi && (unsigned)w < (unsigned)g.Wi;
+      const uint32_t voff = ok ? (uint32_t)(q_off[i] + tapoff) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qsrd, (__attribute__((address_space(3))) void*)(q + (8 * (4 * i + wave)) * ROWB),
+                                               16, voff, 0, 0, 0);
     }
-    const int kp = kt * BK + lvec * C::VEC;
+    const uint32_t kb = (uint32_t)(k * C::ES);
+    const bool k_ok = k < a.Kg;
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
-      const int n = n0 + lrow + 32 * i;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (n < a.Nout && kp < a.Kg) v = *(const u32x4*)(wbase + ((size_t)n * a.Kg + kp));
-      preg[i] = v;
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* q = smem + buf * (TILE_Q + TILE_P);
-    char* p = q + TILE_Q;
-#pragma unroll
-    for (int i = 0; i < QV; ++i) {
-      const int row = lrow + 32 * i;
-      *(u32x4*)(q + row * ROWB + nt_swz(row, lvec) * 16) = qreg[i];
-    }
-#pragma unroll
-    for (int i = 0; i < PV; ++i) {
-      const int row = lrow + 32 * i;
-      *(u32x4*)(p + row * ROWB + nt_swz(row, lvec) * 16) = preg[i];
+      const uint32_t voff = k_ok ? p_off[i] + kb : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(psrd, (__attribute__((address_space(3))) void*)(p + (8 * (4 * i + wave)) * ROWB),
+                                               16, voff, 0, 0, 0);
     }
   };
 
@@ -202,16 +227,22 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  __syncthreads();  // taptab
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nkt) issue(s, s);
+  if (nkt >= STAGES - 1) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) load_tile(kt + 1);
-    const char* q = smem + cur * (TILE_Q + TILE_P);
+    const int cur = kt % STAGES;
+    const bool more = kt + STAGES - 1 < nkt;
+    if (more) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* q = smem + cur * STAGE;
     const char* p = q + TILE_Q;
 #pragma unroll
     for (int sub = 0; sub < BK / C::KSUB; ++sub) {
@@ -250,12 +281,31 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
       }
     }
-    if (kt + 1 < nkt) store_tile(cur ^ 1);
-    __syncthreads();
+    // retire tile kt+1 (leave the younger tiles in flight), then let every wave see it
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
   }
 
   // epilogue: lane holds out[m][n..n+3]
   T* __restrict__ out = (T*)a.out;
+  size_t orow[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WM + 16 * i + fr;
+    if (a.os == 1) {
+      orow[i] = (size_t)m;
+    } else {
+      const int n = (int)fdiv((uint32_t)m, g.fd_hw);
+      const int rem = m - n * g.Ho * g.Wo;
+      const int oi = (int)fdiv((uint32_t)rem, g.fd_w);
+      const int oj = rem - oi * g.Wo;
+      orow[i] = ((size_t)n * a.oH + oi * a.os + a.oph) * a.oW + oj * a.os + a.opw;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WN + 16 * j + 4 * fq;
@@ -263,7 +313,7 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + wm * WM + 16 * i + fr;
-      if (m < g.M) store4(out + (size_t)m * a.Nout + n, acc[j][i]);
+      if (m < g.M) store4(out + orow[i] * a.Nout + n, acc[j][i]);
     }
   }
 }
@@ -276,7 +326,10 @@ __device__ __forceinline__ int tn_swz(int row, int win) {
   return win ^ (((row & 3) | (((row >> 3) & 1) << 2)) & (NWIN - 1));
 }
 
-template <typename T, int BM, int BN, int WAVES_M, int WAVES_N>
+// LDS-DMA ring like the NT kernel: one wave-instruction fills 1 KiB = 1024/ROWB pixel rows; lane
+// l lands in physical 16-B chunk l % (ROWB/16) of its row and loads the logical chunk given by the
+// inverse 32-B-window swizzle, so the transposing fragment reads below stay conflict-light.
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
 __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   using C = Cfg<T>;
   constexpr int BK = 128 / C::ES;  // pixels per k tile (64 bf16 / 32 f32)
@@ -284,72 +337,61 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int QROWB = BM * C::ES, PROWB = BN * C::ES;  // bytes per LDS row
   constexpr int QNW = QROWB / 32, PNW = PROWB / 32;      // 32-B windows per row
-  constexpr int QVR = BM / C::VEC, PVR = BN / C::VEC;    // 16-B vectors per row
-  constexpr int QRPT = BK * QVR / 256, PRPT = BK * PVR / 256;  // rows per thread per tile
-  constexpr int TILE_Q = BK * QROWB, TILE_P = BK * PROWB;
-  static_assert(QRPT >= 1 && PRPT >= 1, "tile too small");
-  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_Q + TILE_P)];
+  constexpr int QCPR = QROWB / 16, PCPR = PROWB / 16;    // 16-B chunks per row
+  constexpr int QRPI = 1024 / QROWB, PRPI = 1024 / PROWB;  // rows per wave-instruction
+  constexpr int QI = BK / QRPI / 4, PI = BK / PRPI / 4;    // instructions per wave per tile
+  constexpr int PER_TILE = QI + PI;
+  static_assert(QI >= 1 && PI >= 1, "tile too small for 4 waves");
+  constexpr int TILE_Q = BK * QROWB, TILE_P = BK * PROWB, STAGE = TILE_Q + TILE_P;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
   const Gather& g = a.g;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int tile_m = blockIdx.x / a.ntn, tile_n = blockIdx.x % a.ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;  // m: kout, n: (tap, c)
   const int p_begin = blockIdx.y * a.kchunk;
   const int p_end = min(p_begin + a.kchunk, g.M);
 
-  // Q (dY) loads: row = tid / QVR + (256/QVR) * i, vec = tid % QVR
-  const int qrow0 = tid / QVR, qvec = tid % QVR;
-  const int prow0 = tid / PVR, pvec = tid % PVR;
-  const int qcol = m0 + qvec * C::VEC;                // kout
-  const bool qcol_ok = qcol < a.Kout;
-  const int pcol = n0 + pvec * C::VEC;                // (tap, c)
-  const int ptap = pcol >> g.log2Ci, pc = pcol & (g.Ci - 1);
-  const bool pcol_ok = pcol < a.Ng;
-  const int pr = pcol_ok ? ptap / g.S : 0, ps = pcol_ok ? ptap - (ptap / g.S) * g.S : 0;
-  const int pdh = pr * g.ks, pdw = ps * g.ks;
-
   const T* __restrict__ dyb = (const T*)a.dy;
   const T* __restrict__ xb = (const T*)g.base;
-  u32x4 qreg[QRPT], preg[PRPT];
-  auto load_tile = [&](int pix0) {
+  // per lane: row within its instruction and physical chunk
+  const int qr = lane / QCPR, qc = lane % QCPR;
+  const int pr = lane / PCPR, pc = lane % PCPR;
+
+  auto issue = [&](int kt, int stage) {
+    char* q = smem + stage * STAGE;
+    char* p = q + TILE_Q;
+    const int pix0 = p_begin + kt * BK;
 #pragma unroll
-    for (int i = 0; i < QRPT; ++i) {
-      const int px = pix0 + qrow0 + (256 / QVR) * i;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (qcol_ok && px < p_end) v = *(const u32x4*)(dyb + ((size_t)px * a.Kout + qcol));
-      qreg[i] = v;
+    for (int i = 0; i < QI; ++i) {
+      const int row = (i * 4 + wave) * QRPI + qr;
+      const int lch = 2 * tn_swz<QNW>(row, qc >> 1) + (qc & 1);  // logical chunk
+      const int px = pix0 + row, col = m0 + lch * C::VEC;
+      const bool ok = px < p_end && col < a.Kout;
+      const void* src = ok ? (const void*)(dyb + ((size_t)px * a.Kout + col)) : (const void*)g_zero16;
+      glds16(src, q + (i * 4 + wave) * QRPI * QROWB);
     }
 #pragma unroll
-    for (int i = 0; i < PRPT; ++i) {
-      const int px = pix0 + prow0 + (256 / PVR) * i;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (pcol_ok && px < p_end) {
+    for (int i = 0; i < PI; ++i) {
+      const int row = (i * 4 + wave) * PRPI + pr;
+      const int lch = 2 * tn_swz<PNW>(row, pc >> 1) + (pc & 1);
+      const int px = pix0 + row, col = n0 + lch * C::VEC;
+      bool ok = px < p_end && col < a.Ng;
+      const void* src = (const void*)g_zero16;
+      if (ok) {
+        const int tap = col >> g.log2Ci, c = col & (g.Ci - 1);
+        const int tr = (int)fdiv((uint32_t)tap, g.fd_s), ts = tap - tr * g.S;
         const int n = (int)fdiv((uint32_t)px, g.fd_hw);
         const int rem = px - n * g.Ho * g.Wo;
         const int oh = (int)fdiv((uint32_t)rem, g.fd_w);
         const int ow = rem - oh * g.Wo;
-        const int h = oh * g.ms + g.off + pdh, w = ow * g.ms + g.off + pdw;
+        const int h = oh * g.ms + g.off_h + tr * g.ks, w = ow * g.ms + g.off_w + ts * g.ks;
         if (h >= 0 && h < g.Hi && w >= 0 && w < g.Wi)
-          v = *(const u32x4*)(xb + ((size_t)((n * g.Hi + h) * g.Wi + w) * g.Ci + pc));
+          src = (const void*)(xb + ((size_t)((n * g.Hi + h) * g.Wi + w) * g.Ci + c));
       }
-      preg[i] = v;
-    }
-  };
-  auto store_tile = [&](int buf) {
-    char* q = smem + buf * (TILE_Q + TILE_P);
-    char* p = q + TILE_Q;
-#pragma unroll
-    for (int i = 0; i < QRPT; ++i) {
-      const int row = qrow0 + (256 / QVR) * i;
-      const int cb = qvec * 16;
-      *(u32x4*)(q + row * QROWB + tn_swz<QNW>(row, cb >> 5) * 32 + (cb & 31)) = qreg[i];
-    }
-#pragma unroll
-    for (int i = 0; i < PRPT; ++i) {
-      const int row = prow0 + (256 / PVR) * i;
-      const int cb = pvec * 16;
-      *(u32x4*)(p + row * PROWB + tn_swz<PNW>(row, cb >> 5) * 32 + (cb & 31)) = preg[i];
+      glds16(src, p + (i * 4 + wave) * PRPI * PROWB);
     }
   };
 
@@ -360,45 +402,54 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
     for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (p_end - p_begin + BK - 1) / BK;
-  if (nkt > 0) {
-    load_tile(p_begin);
-    store_tile(0);
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nkt) issue(s, s);
+  if (nkt >= STAGES - 1) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __syncthreads();
+  __builtin_amdgcn_s_barrier();
+
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) load_tile(p_begin + (kt + 1) * BK);
-    const char* q = smem + cur * (TILE_Q + TILE_P);
+    const int cur = kt % STAGES;
+    const bool more = kt + STAGES - 1 < nkt;
+    if (more) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const char* q = smem + cur * STAGE;
     const char* p = q + TILE_Q;
 #pragma unroll
     for (int sub = 0; sub < BK / C::KSUB; ++sub) {
       if constexpr (C::ES == 2) {
         bf16x8 pf[TN], qf[TM];
+        s16x4 plo[TN], phi[TN], qlo[TM], qhi[TM];
         // lane (fq, fr): rows k = 32 sub + 8 fq + (fr>>2) (+4), cols c0 + 4 (fr&3)
         const int krow = 32 * sub + 8 * fq + (fr >> 2);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int cb = (wn * WN + 16 * j + 4 * (fr & 3)) * 2;
           const int r0 = krow, r1 = krow + 4;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(p + r0 * PROWB + tn_swz<PNW>(r0, cb >> 5) * 32 + (cb & 31)));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(p + r1 * PROWB + tn_swz<PNW>(r1, cb >> 5) * 32 + (cb & 31)));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
-          const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          pf[j] = __builtin_bit_cast(bf16x8, v);
+          plo[j] = ds_read_tr16(lds_addr(p + r0 * PROWB + tn_swz<PNW>(r0, cb >> 5) * 32 + (cb & 31)));
+          phi[j] = ds_read_tr16(lds_addr(p + r1 * PROWB + tn_swz<PNW>(r1, cb >> 5) * 32 + (cb & 31)));
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int cb = (wm * WM + 16 * i + 4 * (fr & 3)) * 2;
           const int r0 = krow, r1 = krow + 4;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(q + r0 * QROWB + tn_swz<QNW>(r0, cb >> 5) * 32 + (cb & 31)));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(q + r1 * QROWB + tn_swz<QNW>(r1, cb >> 5) * 32 + (cb & 31)));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
-          const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          qlo[i] = ds_read_tr16(lds_addr(q + r0 * QROWB + tn_swz<QNW>(r0, cb >> 5) * 32 + (cb & 31)));
+          qhi[i] = ds_read_tr16(lds_addr(q + r1 * QROWB + tn_swz<QNW>(r1, cb >> 5) * 32 + (cb & 31)));
+        }
+        tr_wait();
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const s16x8 v = {plo[j][0], plo[j][1], plo[j][2], plo[j][3], phi[j][0], phi[j][1], phi[j][2], phi[j][3]};
+          pf[j] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const s16x8 v = {qlo[i][0], qlo[i][1], qlo[i][2], qlo[i][3], qhi[i][0], qhi[i][1], qhi[i][2], qhi[i][3]};
           qf[i] = __builtin_bit_cast(bf16x8, v);
         }
 #pragma unroll
@@ -424,8 +475,12 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
       }
     }
-    if (kt + 1 < nkt) store_tile(cur ^ 1);
-    __syncthreads();
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
   }
 
   // epilogue: slab[split][kout = m][n..n+3]
@@ -530,8 +585,8 @@ __global__ void im2col_kernel(const T* __restrict__ x, int N, int H, int W, int 
 
 // w_kcrs f32 -> w_krsc (T) [K][R][S][C] (or [K][Kp] im2col layout), w_crsk (T) [C][R][S][K]
 template <typename T>
-__global__ void pack_weight_kernel(const float* __restrict__ w, int K, int C, int R, int S, int im2col, int Kp,
-                                   T* __restrict__ krsc, T* __restrict__ crsk) {
+__global__ void pack_weight_kernel(const float* __restrict__ w, int K, int C, int R, int S, int st, int pad,
+                                   int im2col, int Kp, T* __restrict__ krsc, T* __restrict__ crsk) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   const int rowlen = im2col ? Kp : R * S * C;
   if (krsc && idx < K * rowlen) {
@@ -544,10 +599,98 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, int K, int C, in
     krsc[idx] = (T)v;
   }
   if (crsk && idx < C * R * S * K) {
-    const int k = idx % K;
-    const int tap = (idx / K) % (R * S);
-    const int c = idx / (K * R * S);
-    crsk[idx] = (T)w[((size_t)k * C + c) * R * S + tap];
+    // [C][R][S][K] for stride 1; for stride st the st*st parity classes (ph,pw) back to back, each
+    // [C][Rc][Sc][K] with taps r = r0 + st*t, r0 = (ph + pad) % st (see sqr_conv2d_bwd_data)
+    int rem = idx, ph = 0, pw = 0, r0 = 0, s0 = 0, Rc = R, Sc = S;
+    for (ph = 0; ph < st; ++ph) {
+      for (pw = 0; pw < st; ++pw) {
+        r0 = (ph + pad) % st;
+        s0 = (pw + pad) % st;
+        Rc = r0 < R ? (R - r0 + st - 1) / st : 0;
+        Sc = s0 < S ? (S - s0 + st - 1) / st : 0;
+        const int sz = C * Rc * Sc * K;
+        if (rem < sz) goto found;
+        rem -= sz;
+      }
+    }
+    return;
+  found:
+    const int k = rem % K;
+    const int u = (rem / K) % Sc;
+    const int t = (rem / (K * Sc)) % Rc;
+    const int c = rem / (K * Sc * Rc);
+    crsk[idx] = (T)w[((size_t)k * C + c) * R * S + (r0 + st * t) * S + (s0 + st * u)];
+  }
+}
+
+struct PackJob {
+  const float* w;
+  void* krsc;
+  void* crsk;
+  int K, C, R, S, st, pad, im2col, Kp, dtype, total;  // total = K*C*R*S source elements
+  FastDiv fd_s, fd_r, fd_c;
+  int cls_off[4], cls_rc[4], cls_sc[4], cls_r0[4], cls_s0[4];  // dgrad parity classes (st <= 2)
+};
+struct PackJobs {  // by value as the kernel argument: 20 * 180 B < the 4 KiB argument limit
+  PackJob j[20];
+};
+
+// pack kernels: one block per (output row, job).  The job's source rows are staged in LDS with
+// coalesced fp32 reads and written back in destination order with coalesced stores.
+// krsc: block = output channel k: w[k][c][tap] (C*RS floats) -> krsc[k][tap][c] (or im2col [k][Kp]).
+template <typename T>
+__device__ void pack_krsc_row(const PackJob& jb, int k, float* lds) {
+  const int RS = jb.R * jb.S, CRS = jb.C * RS;
+  const float* __restrict__ src = jb.w + (size_t)k * CRS;
+  for (int i = threadIdx.x; i < CRS; i += 256) lds[i] = src[i];
+  __syncthreads();
+  const int rowlen = jb.im2col ? jb.Kp : CRS;
+  T* __restrict__ dst = (T*)jb.krsc + (size_t)k * rowlen;
+  for (int j = threadIdx.x; j < rowlen; j += 256) {
+    float v = 0.f;
+    if (j < CRS) {
+      const int tap = j / jb.C, c = j - tap * jb.C;
+      v = lds[c * RS + tap];
+    }
+    dst[j] = (T)v;
+  }
+}
+// crsk: block = input channel c: gathers w[k][c][tap] for all (k, tap) and writes, per parity
+// class, crsk[cls][c][t][u][k] (k innermost -> coalesced)
+template <typename T>
+__device__ void pack_crsk_row(const PackJob& jb, int c, float* lds) {
+  const int RS = jb.R * jb.S, K = jb.K;
+  for (int i = threadIdx.x; i < K * RS; i += 256) {
+    const int k = i / RS, tap = i - k * RS;
+    lds[tap * K + k] = jb.w[((size_t)k * jb.C + c) * RS + tap];
+  }
+  __syncthreads();
+  const int st = jb.st;
+  for (int cl = 0; cl < st * st; ++cl) {
+    const int Rc = jb.cls_rc[cl], Sc = jb.cls_sc[cl];
+    T* __restrict__ dst = (T*)jb.crsk + jb.cls_off[cl] + (size_t)c * Rc * Sc * K;
+    for (int i = threadIdx.x; i < Rc * Sc * K; i += 256) {
+      const int k = i % K, tu = i / K;
+      const int t = tu / Sc, u = tu - t * Sc;
+      const int tap = (jb.cls_r0[cl] + st * t) * jb.S + (jb.cls_s0[cl] + st * u);
+      dst[i] = (T)lds[tap * K + k];
+    }
+  }
+}
+
+// grid (max(K, C), jobs, 2): z = 0 -> krsc rows, z = 1 -> crsk rows.  LDS: max(C*RS, K*RS) floats.
+__global__ void __launch_bounds__(256) pack_weights_batched_kernel(PackJobs jobs) {
+  extern __shared__ float plds[];
+  const PackJob& jb = jobs.j[blockIdx.y];
+  const int row = blockIdx.x;
+  if (blockIdx.z == 0) {
+    if (!jb.krsc || row >= jb.K) return;
+    if (jb.dtype == SQR_DTYPE_BF16) pack_krsc_row<bf16>(jb, row, plds);
+    else pack_krsc_row<float>(jb, row, plds);
+  } else {
+    if (!jb.crsk || row >= jb.C) return;
+    if (jb.dtype == SQR_DTYPE_BF16) pack_crsk_row<bf16>(jb, row, plds);
+    else pack_crsk_row<float>(jb, row, plds);
   }
 }
 
@@ -588,6 +731,9 @@ int check_desc(const sqr_conv_desc* d, Shape* sh) {
   const long long Min = (long long)d->N * d->H * d->W;
   SQR_CHECK_ARG(M < (1ll << 31) && Min < (1ll << 31), "conv2d: too many pixels");
   SQR_CHECK_ARG(d->C >= 8 || M * 64 < (1ll << 31), "conv2d: too many pixels for the im2col path");
+  // 32-bit buffer offsets: every operand tensor must stay below 2 GiB
+  SQR_CHECK_ARG(Min * d->C * 4 < (1ll << 31) && M * d->K * 4 < (1ll << 31) && M * 512 * 4 < (1ll << 32),
+                "conv2d: tensors larger than 2 GiB are not supported");
   sh->M = (int)M;
   sh->im2col = d->C < 8;
   sh->Kp = 64;  // im2col K: next power of two >= max(64, R*S*C) (the gather needs a power-of-2 row)
@@ -599,8 +745,8 @@ int check_desc(const sqr_conv_desc* d, Shape* sh) {
   return 0;
 }
 
-Gather make_gather(const void* base, int Hi, int Wi, int Ci, int Ho, int Wo, int ms, int off, int div, int ks,
-                   int R, int S, int N) {
+Gather make_gather(const void* base, int Hi, int Wi, int Ci, int Ho, int Wo, int ms, int off_h, int off_w, int ks,
+                   int R, int S, int N, int es) {
   Gather g;
   g.base = base;
   g.Hi = Hi;
@@ -610,14 +756,16 @@ Gather make_gather(const void* base, int Hi, int Wi, int Ci, int Ho, int Wo, int
   g.Ho = Ho;
   g.Wo = Wo;
   g.ms = ms;
-  g.off = off;
-  g.div = div;
+  g.off_h = off_h;
+  g.off_w = off_w;
   g.ks = ks;
   g.R = R;
   g.S = S;
   g.M = N * Ho * Wo;
   g.fd_hw = make_fastdiv((uint32_t)(Ho * Wo));
   g.fd_w = make_fastdiv((uint32_t)Wo);
+  g.fd_s = make_fastdiv((uint32_t)S);
+  g.bytes = (uint32_t)((size_t)N * Hi * Wi * Ci * es);
   return g;
 }
 
@@ -636,10 +784,10 @@ int launch_nt(NTArgs a, hipStream_t st) {
   a.ntn = (N + bn - 1) / bn;
   const dim3 grid(a.ntm * a.ntn), blk(256);
   switch (cfg) {
-    case 0: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 2>), grid, blk, 0, st, a); break;
-    case 1: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 64, 4, 1>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 128, 1, 4>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 64, 2, 2>), grid, blk, 0, st, a); break;
+    case 0: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, a); break;
   }
   SQR_HIP_LAUNCH_CHECK("conv_nt_kernel");
   return 0;
@@ -673,10 +821,10 @@ int launch_tn(TNArgs a, const TNPlan& p, hipStream_t st) {
   a.ntn = p.ntn;
   a.kchunk = p.kchunk;
   const dim3 grid(p.ntm * p.ntn, p.splits), blk(256);
-  if (p.bm == 128 && p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 128, 2, 2>), grid, blk, 0, st, a);
-  else if (p.bm == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 64, 4, 1>), grid, blk, 0, st, a);
-  else if (p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 64, 128, 1, 4>), grid, blk, 0, st, a);
-  else hipLaunchKernelGGL((conv_tn_kernel<T, 64, 64, 2, 2>), grid, blk, 0, st, a);
+  if (p.bm == 128 && p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, a);
+  else if (p.bm == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, a);
+  else if (p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((conv_tn_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, a);
   SQR_HIP_LAUNCH_CHECK("conv_tn_kernel");
   return 0;
 }
@@ -719,10 +867,10 @@ extern "C" int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* 
   hipStream_t st = as_stream(stream);
   if (d->dtype == SQR_DTYPE_BF16)
     hipLaunchKernelGGL((pack_weight_kernel<bf16>), dim3(blocks), dim3(256), 0, st, w_kcrs, d->K, d->C, d->R, d->S,
-                       (int)sh.im2col, sh.Kp, (bf16*)w_krsc, (bf16*)w_crsk);
+                       d->stride, d->pad, (int)sh.im2col, sh.Kp, (bf16*)w_krsc, (bf16*)w_crsk);
   else
     hipLaunchKernelGGL((pack_weight_kernel<float>), dim3(blocks), dim3(256), 0, st, w_kcrs, d->K, d->C, d->R,
-                       d->S, (int)sh.im2col, sh.Kp, (float*)w_krsc, (float*)w_crsk);
+                       d->S, d->stride, d->pad, (int)sh.im2col, sh.Kp, (float*)w_krsc, (float*)w_crsk);
   SQR_HIP_LAUNCH_CHECK("pack_weight_kernel");
   return 0;
 }
@@ -748,6 +896,10 @@ extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const 
   a.w = w_krsc;
   a.Nout = d->K;
   a.out = y;
+  a.os = 1;
+  a.oph = a.opw = 0;
+  a.oH = sh.Ho;
+  a.oW = sh.Wo;
   if (sh.im2col) {
     const size_t need = sqr_conv2d_workspace_bytes(d, 0);
     if (workspace_bytes < need || !workspace) {
@@ -756,13 +908,31 @@ extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const 
     }
     rc = d->dtype == SQR_DTYPE_BF16 ? im2col<bf16>(x, d, sh, workspace, st) : im2col<float>(x, d, sh, workspace, st);
     if (rc) return rc;
-    a.g = make_gather(workspace, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 1, 1, 1, 1, d->N);
+    a.g = make_gather(workspace, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 0, 1, 1, 1, d->N, sh.ES);
     a.Kg = sh.Kp;
   } else {
-    a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, 1, 1, d->R, d->S, d->N);
+    a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, -d->pad, 1, d->R, d->S, d->N, sh.ES);
     a.Kg = d->R * d->S * d->C;
   }
   return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
+}
+
+// dgrad parity class (ph, pw) of a stride-st conv: taps r = r0 + st*t with (ph + pad - r) % st == 0
+struct DgradClass {
+  int r0, Rc, s0, Sc, Hc, Wc, off_h, off_w;
+};
+static DgradClass dgrad_class(const sqr_conv_desc* d, int ph, int pw) {
+  DgradClass c;
+  const int st = d->stride;
+  c.r0 = (ph + d->pad) % st;
+  c.s0 = (pw + d->pad) % st;
+  c.Rc = c.r0 < d->R ? (d->R - c.r0 + st - 1) / st : 0;
+  c.Sc = c.s0 < d->S ? (d->S - c.s0 + st - 1) / st : 0;
+  c.Hc = ph < d->H ? (d->H - ph + st - 1) / st : 0;
+  c.Wc = pw < d->W ? (d->W - pw + st - 1) / st : 0;
+  c.off_h = (ph + d->pad - c.r0) / st;
+  c.off_w = (pw + d->pad - c.s0) / st;
+  return c;
 }
 
 extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
@@ -774,15 +944,33 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
   if (rc) return rc;
   SQR_CHECK_ARG(!sh.im2col, "conv2d_bwd_data: C=%d < 8 not supported", d->C);
   SQR_CHECK_ARG(dy && w_crsk && dx, "conv2d_bwd_data: null pointer");
-  NTArgs a;
-  // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+p-r)/st,(w+p-s)/st,k] W[k,c,r,s]
-  a.g = make_gather(dy, sh.Ho, sh.Wo, d->K, d->H, d->W, 1, d->pad, d->stride, -1, d->R, d->S, d->N);
-  a.w = w_crsk;
-  a.Nout = d->C;
-  a.Kg = d->R * d->S * d->K;
-  a.out = dx;
   hipStream_t st = as_stream(stream);
-  return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
+  // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+p-r)/st,(w+p-s)/st,k] W[k,c,r,s] over the divisible taps.
+  // Output pixels split by parity (h%st, w%st); in class (ph,pw) only taps r = r0 + st*t contribute
+  // and dY row = i + off_h - t: a stride-1 implicit GEMM over the class grid (Hc x Wc).
+  const char* wp = (const char*)w_crsk;
+  for (int ph = 0; ph < d->stride; ++ph) {
+    for (int pw = 0; pw < d->stride; ++pw) {
+      const DgradClass c = dgrad_class(d, ph, pw);
+      if (c.Hc == 0 || c.Wc == 0) continue;
+      NTArgs a;
+      a.g = make_gather(dy, sh.Ho, sh.Wo, d->K, c.Hc, c.Wc, 1, c.off_h, c.off_w, -1, c.Rc > 0 ? c.Rc : 1,
+                        c.Sc > 0 ? c.Sc : 1, d->N, sh.ES);
+      a.w = wp;
+      a.Nout = d->C;
+      a.Kg = c.Rc * c.Sc * d->K;  // 0 -> the class receives no gradient: zeros are written
+      a.out = dx;
+      a.os = d->stride;
+      a.oph = ph;
+      a.opw = pw;
+      a.oH = d->H;
+      a.oW = d->W;
+      rc = d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
+      if (rc) return rc;
+      wp += (size_t)d->C * c.Rc * c.Sc * d->K * sh.ES;
+    }
+  }
+  return 0;
 }
 
 static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, float* dw_kcrs,
@@ -810,10 +998,10 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
       col = ws;
       ws += colb;
     }
-    a.g = make_gather(col, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 1, 1, 1, 1, d->N);
+    a.g = make_gather(col, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 0, 1, 1, 1, d->N, sh.ES);
     Ng = sh.Kp;
   } else {
-    a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, 1, 1, d->R, d->S, d->N);
+    a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, -d->pad, 1, d->R, d->S, d->N, sh.ES);
     Ng = d->R * d->S * d->C;
   }
   a.dy = dy;
@@ -838,4 +1026,63 @@ extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kc
 extern "C" int sqr_conv2d_bwd_weight_col(const void* col, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                                          void* workspace, size_t workspace_bytes, void* stream) {
   return bwd_weight_impl(nullptr, col, dy, dw_kcrs, d, workspace, workspace_bytes, stream);
+}
+
+extern "C" int sqr_conv2d_pack_weights(const sqr_pack_job* jobs, int njobs, void* stream) {
+  SQR_CHECK_ARG(jobs && njobs >= 0 && njobs <= 20, "conv2d_pack_weights: 0 <= njobs <= 20 required");
+  if (njobs == 0) return 0;
+  PackJobs pj;
+  int maxtot = 0, maxlds = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const sqr_conv_desc* d = &jobs[i].desc;
+    SQR_CHECK_ARG(jobs[i].w_kcrs && (jobs[i].w_krsc || jobs[i].w_crsk), "conv2d_pack_weights: job %d null", i);
+    SQR_CHECK_ARG(d->K >= 1 && d->C >= 1 && d->R >= 1 && d->S >= 1 && d->stride >= 1 && d->stride <= 2 &&
+                      d->pad >= 0,
+                  "conv2d_pack_weights: job %d bad dims (stride <= 2)", i);
+    SQR_CHECK_ARG(d->dtype == SQR_DTYPE_F32 || d->dtype == SQR_DTYPE_BF16, "conv2d_pack_weights: bad dtype");
+    const int im2col = d->C < 8;
+    SQR_CHECK_ARG(!(im2col && jobs[i].w_crsk), "conv2d_pack_weights: no dgrad weights for C<8 convs");
+    int kp = 64;
+    while (kp < d->R * d->S * d->C) kp *= 2;
+    PackJob& j = pj.j[i];
+    j.w = jobs[i].w_kcrs;
+    j.krsc = jobs[i].w_krsc;
+    j.crsk = jobs[i].w_crsk;
+    j.K = d->K;
+    j.C = d->C;
+    j.R = d->R;
+    j.S = d->S;
+    j.st = d->stride;
+    j.pad = d->pad;
+    j.im2col = im2col;
+    j.Kp = kp;
+    j.dtype = d->dtype;
+    j.total = d->K * d->C * d->R * d->S;
+    j.fd_s = make_fastdiv(d->S);
+    j.fd_r = make_fastdiv(d->R);
+    j.fd_c = make_fastdiv(d->C);
+    int off = 0;
+    for (int ph = 0; ph < d->stride; ++ph)
+      for (int pw = 0; pw < d->stride; ++pw) {
+        const int cl = ph * d->stride + pw;
+        const int r0 = (ph + d->pad) % d->stride, s0 = (pw + d->pad) % d->stride;
+        const int rc = r0 < d->R ? (d->R - r0 + d->stride - 1) / d->stride : 0;
+        const int sc = s0 < d->S ? (d->S - s0 + d->stride - 1) / d->stride : 0;
+        j.cls_off[cl] = off;
+        j.cls_r0[cl] = r0;
+        j.cls_s0[cl] = s0;
+        j.cls_rc[cl] = rc;
+        j.cls_sc[cl] = sc;
+        off += d->C * rc * sc * d->K;
+      }
+    const int rows = d->K > d->C ? d->K : d->C;
+    maxtot = rows > maxtot ? rows : maxtot;
+    const int lds = (d->K > d->C ? d->K : d->C) * d->R * d->S;
+    maxlds = lds > maxlds ? lds : maxlds;
+  }
+  SQR_CHECK_ARG(maxlds * 4 <= 160 * 1024, "conv2d_pack_weights: weight rows too large for LDS staging");
+  hipLaunchKernelGGL(pack_weights_batched_kernel, dim3(maxtot, njobs, 2), dim3(256), (size_t)maxlds * 4,
+                     as_stream(stream), pj);
+  SQR_HIP_LAUNCH_CHECK("pack_weights_batched_kernel");
+  return 0;
 }

@@ -24,6 +24,10 @@ class SqrConvDesc(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("N", "C", "H", "W", "K", "R", "S", "stride", "pad", "dtype")]
 
 
+class SqrPackJob(ctypes.Structure):
+    _fields_ = [("w_kcrs", c_void_p), ("desc", SqrConvDesc), ("w_krsc", c_void_p), ("w_crsk", c_void_p)]
+
+
 # name -> (restype, argtypes); must mirror include/sqr.h exactly
 SIGNATURES = {
     "sqr_version": (c_int, []),
@@ -39,6 +43,7 @@ SIGNATURES = {
     "sqr_conv2d_out_hw": (c_int, [ctypes.POINTER(SqrConvDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "sqr_conv2d_workspace_bytes": (c_size_t, [ctypes.POINTER(SqrConvDesc), c_int]),
     "sqr_conv2d_pack_weight": (c_int, [c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_void_p, c_void_p]),
+    "sqr_conv2d_pack_weights": (c_int, [ctypes.POINTER(SqrPackJob), c_int, c_void_p]),
     "sqr_conv2d_fwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t,
                                c_void_p]),
     "sqr_conv2d_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,

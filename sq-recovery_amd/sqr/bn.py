@@ -87,10 +87,18 @@ class BNActFn(torch.autograd.Function):
         return dx, dgamma, dbeta, None, None, dres, None, None, None, None
 
 
-def bn_act(x, bn, residual=None, relu=True):
+def count_batches(bns):
+    """num_batches_tracked += 1 for every training-mode BN of a model forward in ONE foreach
+    launch (instead of one tiny kernel per layer); the bn_act/stem calls then pass counted=True."""
+    t = [b.num_batches_tracked for b in bns if b.training and b.track_running_stats]
+    if t:
+        torch._foreach_add_(t, 1)
+
+
+def bn_act(x, bn, residual=None, relu=True, counted=False):
     """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics."""
     training = bn.training or not bn.track_running_stats
-    if training and bn.track_running_stats:
+    if training and bn.track_running_stats and not counted:
         bn.num_batches_tracked.add_(1)
     mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
     rm = bn.running_mean if bn.track_running_stats else None
@@ -141,9 +149,9 @@ class StemFn(torch.autograd.Function):
         return dx, dgamma, dbeta, None, None, None, None, None
 
 
-def stem(x, bn):
+def stem(x, bn, counted=False):
     training = bn.training or not bn.track_running_stats
-    if training and bn.track_running_stats:
+    if training and bn.track_running_stats and not counted:
         bn.num_batches_tracked.add_(1)
     mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
     rm = bn.running_mean if bn.track_running_stats else None

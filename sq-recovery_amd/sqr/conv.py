@@ -11,7 +11,7 @@ Compute dtype: bfloat16 when the input is bf16 or CUDA autocast is on with bf16,
 import torch
 import torch.nn as nn
 
-from ._lib import SqrConvDesc, check, lib, ptr, stream_ptr
+from ._lib import SqrConvDesc, SqrPackJob, check, lib, ptr, stream_ptr
 
 DT_F32, DT_BF16 = 0, 1
 _CL = torch.channels_last
@@ -82,6 +82,50 @@ def pack_weight(weight, d, need_crsk):
     return krsc, crsk
 
 
+def _alloc_packed(weight, dt, need_crsk):
+    K, C, R, S = weight.shape
+    if C < 8:
+        kp = 64
+        while kp < R * S * C:
+            kp *= 2
+        krsc = torch.empty(K, kp, dtype=dt, device=weight.device)
+    else:
+        krsc = torch.empty(K, R, S, C, dtype=dt, device=weight.device)
+    crsk = torch.empty(C, R, S, K, dtype=dt, device=weight.device) if (need_crsk and C >= 8) else None
+    return krsc, crsk
+
+
+def pack_all(convs, dtype):
+    """Pack the weights of several sqr Conv2d modules for `dtype` in one launch (called at the
+    start of a model forward; the model clears the modules' caches at its end, see clear_packed).
+    A module's forward uses its cache only if (weight._version, dtype, data_ptr) still match."""
+    jobs = []
+    for m in convs:
+        w = m.weight
+        key = (w._version, dtype, w.data_ptr())
+        krsc, crsk = _alloc_packed(w, dtype, True)
+        K, C, R, S = w.shape
+        d = _desc(1, C, R, R, K, R, S, m.stride[0], m.padding[0], dtype)
+        jobs.append((m, key, w.detach().float().contiguous(), d, krsc, crsk))
+    for i in range(0, len(jobs), 20):
+        chunk = jobs[i:i + 20]
+        arr = (SqrPackJob * len(chunk))()
+        for j, (_, _, w, d, krsc, crsk) in enumerate(chunk):
+            arr[j].w_kcrs = w.data_ptr()
+            arr[j].desc = d
+            arr[j].w_krsc = krsc.data_ptr()
+            arr[j].w_crsk = crsk.data_ptr() if crsk is not None else None
+        check(lib().sqr_conv2d_pack_weights(arr, len(chunk), stream_ptr(chunk[0][2].device)),
+              "sqr_conv2d_pack_weights")
+    for m, key, w, d, krsc, crsk in jobs:
+        m._packed = (key, krsc, crsk, w)
+
+
+def clear_packed(convs):
+    for m in convs:
+        m._packed = None
+
+
 def conv2d_fwd(x, w_krsc, d, return_ws=False):
     """y = conv(x); with return_ws the workspace (holding the im2col matrix for C<8) is returned too."""
     import ctypes
@@ -137,13 +181,16 @@ def compute_dtype(x):
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, dt):
+    def forward(ctx, x, weight, bias, stride, pad, dt, packed):
         N, C, H, W = x.shape
         K, _, R, S = weight.shape
         xin = x.to(dt).contiguous(memory_format=_CL)
         d = _desc(N, C, H, W, K, R, S, stride, pad, dt)
         need_dx = ctx.needs_input_grad[0]
-        krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
+        if packed is not None:
+            krsc, crsk = packed
+        else:
+            krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
         y, ws = conv2d_fwd(xin, krsc, d, return_ws=True)
         if bias is not None:
             y = y + bias.to(dt).view(1, K, 1, 1)
@@ -170,13 +217,13 @@ class Conv2dFn(torch.autograd.Function):
             dw = conv2d_bwd_weight(xin, g, d, col)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0):
+def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None):
     if not x.is_cuda:
         raise ValueError("sqr conv2d runs on MI355X; got a %s tensor" % x.device)
-    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x))
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed)
 
 
 class Conv2d(nn.Conv2d):
@@ -189,6 +236,13 @@ class Conv2d(nn.Conv2d):
                 or self.stride[0] != self.stride[1] or self.padding[0] != self.padding[1]
                 or isinstance(self.padding, str)):
             raise ValueError("sqr Conv2d supports groups=1, dilation=1, symmetric stride/padding only")
+        self._packed = None  # ((weight version, dtype, ptr), krsc, crsk, fp32 source) from pack_all
 
     def forward(self, x):
-        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0])
+        dt = compute_dtype(x) if x.is_cuda else None
+        packed = None
+        if self._packed is not None and dt is not None:
+            key, krsc, crsk, _ = self._packed
+            if key == (self.weight._version, dt, self.weight.data_ptr()):
+                packed = (krsc, crsk)
+        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], packed)

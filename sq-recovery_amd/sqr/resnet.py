@@ -12,8 +12,8 @@ import warnings
 import torch
 import torch.nn as nn
 
-from .bn import bn_act, stem
-from .conv import Conv2d
+from .bn import bn_act, count_batches, stem
+from .conv import Conv2d, clear_packed, compute_dtype, pack_all
 
 
 class BasicBlock(nn.Module):
@@ -31,11 +31,11 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         # conv -> fused [bn+relu] -> conv -> fused [bn + identity + relu]   (libsqr kernels)
-        out = bn_act(self.conv1(x), self.bn1, relu=True)
+        out = bn_act(self.conv1(x), self.bn1, relu=True, counted=True)
         identity = x
         if self.downsample is not None:
-            identity = bn_act(self.downsample[0](x), self.downsample[1], relu=False)
-        return bn_act(self.conv2(out), self.bn2, residual=identity, relu=True)
+            identity = bn_act(self.downsample[0](x), self.downsample[1], relu=False, counted=True)
+        return bn_act(self.conv2(out), self.bn2, residual=identity, relu=True, counted=True)
 
 
 class ResNet18(nn.Module):
@@ -71,8 +71,15 @@ class ResNet18(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = stem(self.conv1(x), self.bn1)  # fused bn1 -> relu -> maxpool
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        convs = [m for m in self.modules() if isinstance(m, Conv2d)]
+        if x.is_cuda:  # pack every conv weight of this step in one launch
+            pack_all(convs, compute_dtype(x))
+        count_batches([m for m in self.modules() if isinstance(m, nn.BatchNorm2d)])
+        try:
+            x = stem(self.conv1(x), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        finally:
+            clear_packed(convs)  # packed weights live on in autograd's saved tensors only
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
