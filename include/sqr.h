@@ -118,6 +118,13 @@ int sqr_conv2d_pack_weights(const sqr_pack_job* jobs, int njobs, void* stream);
  * im2col into the workspace + a 1x1 GEMM; the im2col matrix stays in the workspace). */
 int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, void* workspace,
                    size_t workspace_bytes, void* stream);
+/* Forward that also emits BatchNorm batch-statistics partials of the (dtype-rounded) output:
+ * stats[rows][2][K] f32 = per M-tile (sum, sum of squares) per output channel, *stats_rows = rows.
+ * stats must hold sqr_conv2d_stats_floats(d) floats.  Feed them to sqr_bn_fwd_stats /
+ * sqr_stem_fwd_stats so the BatchNorm that follows the conv never re-reads the activation. */
+size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
+int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
+                         int* stats_rows, void* workspace, size_t workspace_bytes, void* stream);
 /* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1
  * implicit GEMM per output-parity class (no work on structurally zero taps). */
 int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
@@ -143,6 +150,11 @@ int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const float* gamma,
                float* running_mean, float* running_var, float momentum, float eps, int training,
                const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
                void* workspace, size_t workspace_bytes, void* stream);
+/* training-mode sqr_bn_fwd with the batch statistics taken from sqr_conv2d_fwd_stats partials */
+int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, const float* stats, int stats_rows,
+                     const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
+                     float eps, const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
+                     void* workspace, size_t workspace_bytes, void* stream);
 /* backward of sqr_bn_fwd (training statistics): g = dy * [y > 0] (y = the forward output, NULL when
  * the forward had no ReLU); dx, dgamma = sum g*xhat, dbeta = sum g; dres (nullable) = g. */
 int sqr_bn_bwd(const void* dy, const void* y, const void* x, long long M, int C, int dtype, const float* gamma,
@@ -156,6 +168,10 @@ int sqr_stem_fwd(const void* x, int N, int H, int W, int C, int dtype, const flo
                  float* running_mean, float* running_var, float momentum, float eps, int training, void* y,
                  uint8_t* argmax, float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
                  void* stream);
+int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int dtype, const float* stats, int stats_rows,
+                       const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
+                       float eps, void* y, uint8_t* argmax, float* save_mean, float* save_invstd, void* workspace,
+                       size_t workspace_bytes, void* stream);
 /* dpool/ypool [N][Ho][Wo][C] (gradient and value of the pooled output), x = conv1 output. */
 int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t* argmax, const void* x, int N, int H, int W,
                  int C, int dtype, const float* gamma, const float* save_mean, const float* save_invstd, void* dx,

@@ -141,29 +141,36 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
   }
 }
 
-// one wave per channel: lane l sums partials l, l+64, ... then a fixed xor-tree wave reduction
-// (deterministic).  Block = 4 waves = 4 channels; returns false for lanes/channels with nothing to do.
-__device__ __forceinline__ bool sum_partials(const double* __restrict__ part, int nblk, int C, double* s, int* cout) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+// one block per channel: thread t sums partials t, t+256, ... (independent loads in flight), then a
+// fixed xor-tree wave reduction and a fixed-order sum of the 4 waves (deterministic).  Returns
+// true on thread 0 only.
+template <typename P>
+__device__ __forceinline__ bool sum_partials(const P* __restrict__ part, int nblk, int C, double* s, int* cout) {
+  __shared__ double red[2][4];
+  const int c = blockIdx.x, t = threadIdx.x;
   double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int k = lane; k < nblk; k += 64) {
-      a += part[(size_t)k * 2 * C + c];
-      b += part[(size_t)k * 2 * C + C + c];
-    }
+#pragma unroll 4
+  for (int k = t; k < nblk; k += 256) {
+    a += (double)part[(size_t)k * 2 * C + c];
+    b += (double)part[(size_t)k * 2 * C + C + c];
   }
   a = wave_sum_d(a);
   b = wave_sum_d(b);
-  if (lane != 0 || c >= C) return false;
-  s[0] = a;
-  s[1] = b;
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = a;
+    red[1][t >> 6] = b;
+  }
+  __syncthreads();
+  if (t != 0) return false;
+  s[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  s[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   *cout = c;
   return true;
 }
 
 // forward finalize: coef[0][c] = scale, coef[1][c] = shift; save_mean/save_invstd; running stats
-__global__ void fwd_finalize_kernel(const double* __restrict__ part, int nblk, int M, int C,
+template <typename P>
+__global__ void fwd_finalize_kernel(const P* __restrict__ part, int nblk, int M, int C,
                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                     float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
                                     float* __restrict__ save_mean, float* __restrict__ save_invstd,
@@ -340,102 +347,112 @@ __global__ void __launch_bounds__(256) bnrelu_maxpool_fwd_kernel(const T* __rest
   }
 }
 
-// gradient at a full-resolution pixel: sum of dpool over the (<=4) windows whose argmax is this
-// pixel and whose pooled (post-ReLU) value is > 0 — exactly maxpool-backward then ReLU-backward
-// of the unfused graph (the pooled value IS the ReLU output at the argmax pixel).
+// Backward of the stem works on 2x2 quads of full-resolution pixels (2k+py, 2j+px): exactly the
+// pooling windows (k+a, j+b), a,b in {0,1}, touch the quad, window (k+a, j+b) at tap
+// (py-2a+1)*3 + (px-2b+1) (only taps inside the 3x3 window exist).  Each window's (argmax, dpool,
+// ypool) is read once per quad instead of once per pixel.  A pixel's gradient is the sum of dpool
+// over the windows whose argmax it is and whose pooled (post-ReLU) value is > 0 — maxpool-backward
+// then ReLU-backward of the unfused graph (the pooled value IS the ReLU output at the argmax).
 template <typename T>
-__device__ __forceinline__ void stem_grad(const T* __restrict__ dpool, const T* __restrict__ ypool,
-                                          const uint8_t* __restrict__ arg, int n, int h, int w, int v, int C,
-                                          int Ho, int Wo, float* g) {
+__device__ __forceinline__ void stem_quad_grad(const T* __restrict__ dpool, const T* __restrict__ ypool,
+                                               const uint8_t* __restrict__ arg, int n, int k, int j, int v, int C,
+                                               int Ho, int Wo, float (*g)[8]) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) g[k] = 0.f;
-  const int oh0 = h >> 1, oh1 = min(Ho - 1, (h + 1) >> 1);
-  const int ow0 = w >> 1, ow1 = min(Wo - 1, (w + 1) >> 1);
-  for (int oh = oh0; oh <= oh1; ++oh) {
-    const int dh = h - (oh * 2 - 1);
-    for (int ow = ow0; ow <= ow1; ++ow) {
-      const int dw = w - (ow * 2 - 1);
-      const uint64_t tap = (uint64_t)(dh * 3 + dw);
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[q][e] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int oh = k + a, ow = j + b;
+      if (oh >= Ho || ow >= Wo) continue;
       const size_t o = (((size_t)n * Ho + oh) * Wo + ow) * C + v * 8;
-      const uint64_t a = *(const uint64_t*)(arg + o);
+      const uint64_t am = *(const uint64_t*)(arg + o);
       float dp[8], yp[8];
       V8<T>::load(dpool + o, dp);
       V8<T>::load(ypool + o, yp);
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (((a >> (8 * k)) & 0xff) == tap && yp[k] > 0.f) g[k] += dp[k];
+      for (int py = 0; py < 2; ++py) {
+#pragma unroll
+        for (int px = 0; px < 2; ++px) {
+          const int dh = py - 2 * a + 1, dw = px - 2 * b + 1;
+          if (dh < 0 || dw < 0) continue;
+          const uint64_t tap = (uint64_t)(dh * 3 + dw);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((am >> (8 * e)) & 0xff) == tap && yp[e] > 0.f) g[py * 2 + px][e] += dp[e];
+        }
+      }
     }
   }
 }
 
+// per-block f64 partials of (sum g, sum g*(x-mean)) over a contiguous range of quad-vectors
+// (blocks start at multiples of 256 so thread t always owns channel vector t % V)
 template <typename T>
 __global__ void __launch_bounds__(256) stem_bwd_reduce_kernel(const T* __restrict__ dpool,
                                                               const T* __restrict__ ypool,
                                                               const uint8_t* __restrict__ arg,
                                                               const T* __restrict__ x, const float* __restrict__ mean,
                                                               int N, int H, int W, int C, int Ho, int Wo, int chunk,
-                                                              FastDiv fd_w, FastDiv fd_h, double* __restrict__ part) {
+                                                              FastDiv fd_wo, FastDiv fd_ho, double* __restrict__ part) {
   extern __shared__ double red[];
-  const int V = C >> 3, rows = 256 / V;
-  const int tid = threadIdx.x;
-  const int row = tid / V, v = tid - row * V;
-  const int M = N * H * W;
+  const int lv = __builtin_ctz(C >> 3);
+  const int V = C >> 3;
+  const int tid = threadIdx.x, v = tid & (V - 1);
+  const int nqv = (N * Ho * Wo) << lv;
   double sa[8], sb[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.0;
+  for (int e = 0; e < 8; ++e) sa[e] = sb[e] = 0.0;
   float mu[8];
   load8f(mean + v * 8, mu);
-  const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
-  if (row < rows) {
-    constexpr int U = 4;
-    for (int pb = p0 + row; pb < p1; pb += U * rows) {
-      float g[U][8], xv[U][8];
+  const int i0 = blockIdx.x * chunk, i1 = min(i0 + chunk, nqv);
+#pragma unroll 2
+  for (int i = i0 + tid; i < i1; i += 256) {
+    const int qp = i >> lv;
+    const int q2 = (int)fdiv((uint32_t)qp, fd_wo), j = qp - q2 * Wo;
+    const int n = (int)fdiv((uint32_t)q2, fd_ho), k = q2 - n * Ho;
+    float g[4][8];
+    stem_quad_grad<T>(dpool, ypool, arg, n, k, j, v, C, Ho, Wo, g);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int p = pb + u * rows;
-        if (p < p1) {
-          const int q = (int)fdiv((uint32_t)p, fd_w), w = p - q * W;
-          const int n = (int)fdiv((uint32_t)q, fd_h), h = q - n * H;
-          stem_grad<T>(dpool, ypool, arg, n, h, w, v, C, Ho, Wo, g[u]);
-          V8<T>::load(x + (size_t)p * C + v * 8, xv[u]);
-        } else {
+    for (int py = 0; py < 2; ++py) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            g[u][i] = 0.f;
-            xv[u][i] = mu[i];
-          }
+      for (int px = 0; px < 2; ++px) {
+        const int h = 2 * k + py, w = 2 * j + px;
+        if (h >= H || w >= W) continue;
+        float xv[8];
+        V8<T>::load(x + (((size_t)n * H + h) * W + w) * C + v * 8, xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gg = g[py * 2 + px][e];
+          sa[e] += (double)gg;
+          sb[e] += (double)gg * (double)(xv[e] - mu[e]);
         }
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          sa[i] += (double)g[u][i];
-          sb[i] += (double)g[u][i] * (double)(xv[u][i] - mu[i]);
-        }
-    }
-    double* dst = red + ((size_t)row * V + v) * 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      dst[i] = sa[i];
-      dst[8 + i] = sb[i];
     }
   }
+  double* dst = red + (size_t)tid * 16;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    dst[e] = sa[e];
+    dst[8 + e] = sb[e];
+  }
   __syncthreads();
-  if (row == 0) {
-    for (int r = 1; r < rows; ++r) {
+  if (tid < V) {
+    for (int r = 1; r < 256 / V; ++r) {
       const double* src = red + ((size_t)r * V + v) * 16;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        sa[i] += src[i];
-        sb[i] += src[8 + i];
+      for (int e = 0; e < 8; ++e) {
+        sa[e] += src[e];
+        sb[e] += src[8 + e];
       }
     }
     double* out = part + (size_t)blockIdx.x * 2 * C;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      out[v * 8 + i] = sa[i];
-      out[C + v * 8 + i] = sb[i];
+    for (int e = 0; e < 8; ++e) {
+      out[v * 8 + e] = sa[e];
+      out[C + v * 8 + e] = sb[e];
     }
   }
 }
@@ -445,27 +462,34 @@ __global__ void __launch_bounds__(256) stem_bwd_apply_kernel(const T* __restrict
                                                              const T* __restrict__ ypool,
                                                              const uint8_t* __restrict__ arg,
                                                              const T* __restrict__ x, const float* __restrict__ bcoef,
-                                                             int N, int H, int W, int C, int Ho, int Wo, FastDiv fd_w,
-                                                             FastDiv fd_h, T* __restrict__ dx) {
+                                                             int N, int H, int W, int C, int Ho, int Wo,
+                                                             FastDiv fd_wo, FastDiv fd_ho, T* __restrict__ dx) {
   const int lv = __builtin_ctz(C >> 3);
-  const int nvec = N * H * W << lv;
-  {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nvec) return;
-    const int v = i & ((1 << lv) - 1);
-    const int p = i >> lv;
-    const int q = (int)fdiv((uint32_t)p, fd_w), w = p - q * W;
-    const int n = (int)fdiv((uint32_t)q, fd_h), h = q - n * H;
-    float g[8], xv[8], k1[8], k2[8], k3[8];
-    stem_grad<T>(dpool, ypool, arg, n, h, w, v, C, Ho, Wo, g);
-    V8<T>::load(x + i * 8, xv);
-    load8f(bcoef + v * 8, k1);
-    load8f(bcoef + C + v * 8, k2);
-    load8f(bcoef + 2 * C + v * 8, k3);
-    float o[8];
+  const int nqv = (N * Ho * Wo) << lv;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nqv) return;
+  const int v = i & ((1 << lv) - 1);
+  const int qp = i >> lv;
+  const int q2 = (int)fdiv((uint32_t)qp, fd_wo), j = qp - q2 * Wo;
+  const int n = (int)fdiv((uint32_t)q2, fd_ho), k = q2 - n * Ho;
+  float g[4][8], k1[8], k2[8], k3[8];
+  stem_quad_grad<T>(dpool, ypool, arg, n, k, j, v, C, Ho, Wo, g);
+  load8f(bcoef + v * 8, k1);
+  load8f(bcoef + C + v * 8, k2);
+  load8f(bcoef + 2 * C + v * 8, k3);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k3[k], xv[k], k2[k]));
-    V8<T>::store(dx + i * 8, o);
+  for (int py = 0; py < 2; ++py) {
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      const int h = 2 * k + py, w = 2 * j + px;
+      if (h >= H || w >= W) continue;
+      const size_t o = (((size_t)n * H + h) * W + w) * C + v * 8;
+      float xv[8], out[8];
+      V8<T>::load(x + o, xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = fmaf(k1[e], g[py * 2 + px][e], fmaf(k3[e], xv[e], k2[e]));
+      V8<T>::store(dx + o, out);
+    }
   }
 }
 
@@ -518,18 +542,25 @@ extern "C" size_t sqr_bn_workspace_bytes(long long M, int C) {
   return a256((size_t)p.nblk * 2 * C * sizeof(double)) + a256((size_t)3 * C * sizeof(float));
 }
 
+
+
 template <typename T>
 static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const float* beta, float* rmean,
                        float* rvar, float momentum, float eps, int training, const void* res, int relu, void* y,
-                       float* save_mean, float* save_invstd, void* ws, hipStream_t st) {
+                       float* save_mean, float* save_invstd, void* ws, hipStream_t st, const float* ext = nullptr,
+                       int ext_rows = 0) {
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
-  if (training) {
+  if (training && ext) {  // statistics partials produced by the conv epilogue
+    hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, ext, ext_rows, M, C, gamma, beta,
+                       rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
+    SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel(ext)");
+  } else if (training) {
     hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
                        (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("bn reduce_kernel");
-    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+    hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel");
   } else {
@@ -575,7 +606,7 @@ static int bn_bwd_impl(const void* dy, const void* y, const void* x, int M, int 
   hipLaunchKernelGGL((reduce_kernel<T, 1>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)dy,
                      (const T*)y, mean, M, C, p.chunk, part);
   SQR_HIP_LAUNCH_CHECK("bn bwd reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel");
   const int nvec = M * (C / 8);
@@ -611,16 +642,21 @@ extern "C" size_t sqr_stem_workspace_bytes(int N, int H, int W, int C) {
 template <typename T>
 static int stem_fwd_impl(const void* x, int N, int H, int W, int C, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, int training, void* y, uint8_t* arg,
-                         float* save_mean, float* save_invstd, void* ws, hipStream_t st) {
+                         float* save_mean, float* save_invstd, void* ws, hipStream_t st, const float* ext = nullptr,
+                         int ext_rows = 0) {
   const int M = N * H * W;
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
-  if (training) {
+  if (training && ext) {
+    hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, ext, ext_rows, M, C, gamma, beta,
+                       rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
+    SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel(ext)");
+  } else if (training) {
     hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
                        (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("stem reduce_kernel");
-    hipLaunchKernelGGL(fwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+    hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel");
   } else {
@@ -666,16 +702,19 @@ static int stem_bwd_impl(const void* dpool, const void* ypool, const uint8_t* ar
   double* part = (double*)ws;
   float* bcoef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
-  hipLaunchKernelGGL((stem_bwd_reduce_kernel<T>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)dpool,
-                     (const T*)ypool, arg, (const T*)x, mean, N, H, W, C, Ho, Wo, p.chunk, make_fastdiv(W),
-                     make_fastdiv(H), part);
+  const int nqv = N * Ho * Wo * (C / 8);
+  int chunk = (nqv + p.nblk - 1) / p.nblk;
+  chunk = ((chunk + 255) / 256) * 256;
+  const int nblk = (nqv + chunk - 1) / chunk;  // <= p.nblk: the partials fit the workspace
+  hipLaunchKernelGGL((stem_bwd_reduce_kernel<T>), dim3(nblk), dim3(256), (size_t)256 * 16 * sizeof(double), st,
+                     (const T*)dpool, (const T*)ypool, arg, (const T*)x, mean, N, H, W, C, Ho, Wo, chunk,
+                     make_fastdiv(Wo), make_fastdiv(Ho), part);
   SQR_HIP_LAUNCH_CHECK("stem_bwd_reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3((C + 3) / 4), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, bcoef);
   SQR_HIP_LAUNCH_CHECK("stem bwd_finalize_kernel");
-  const long long nvec = (long long)M * (C / 8);
-  hipLaunchKernelGGL((stem_bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dpool,
-                     (const T*)ypool, arg, (const T*)x, bcoef, N, H, W, C, Ho, Wo, make_fastdiv(W), make_fastdiv(H),
+  hipLaunchKernelGGL((stem_bwd_apply_kernel<T>), dim3(ew_grid(nqv)), dim3(256), 0, st, (const T*)dpool,
+                     (const T*)ypool, arg, (const T*)x, bcoef, N, H, W, C, Ho, Wo, make_fastdiv(Wo), make_fastdiv(Ho),
                      (T*)dx);
   SQR_HIP_LAUNCH_CHECK("stem_bwd_apply_kernel");
   return 0;
@@ -699,4 +738,45 @@ extern "C" int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t*
                                workspace, st);
   return stem_bwd_impl<float>(dpool, ypool, argmax, x, N, H, W, C, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
                               workspace, st);
+}
+
+// ---------------------------------------------------------------- with statistics from the conv epilogue
+extern "C" int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, const float* stats, int stats_rows,
+                                const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                float momentum, float eps, const void* residual, int relu, void* y, float* save_mean,
+                                float* save_invstd, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && y && stats && stats_rows > 0 && save_mean && save_invstd && workspace, "bn_fwd_stats: null pointer");
+  if (workspace_bytes < sqr_bn_workspace_bytes(M, C)) {
+    set_error("bn_fwd_stats: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return bn_fwd_impl<bf16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
+                             save_mean, save_invstd, workspace, st, stats, stats_rows);
+  return bn_fwd_impl<float>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
+                            save_mean, save_invstd, workspace, st, stats, stats_rows);
+}
+
+extern "C" int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int dtype, const float* stats,
+                                  int stats_rows, const float* gamma, const float* beta, float* running_mean,
+                                  float* running_var, float momentum, float eps, void* y, uint8_t* argmax,
+                                  float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  int rc = check_mc((long long)N * H * W, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && y && stats && stats_rows > 0 && argmax && save_mean && save_invstd && workspace,
+                "stem_fwd_stats: null pointer");
+  if (workspace_bytes < sqr_stem_workspace_bytes(N, H, W, C)) {
+    set_error("stem_fwd_stats: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return stem_fwd_impl<bf16>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, 1, y, argmax,
+                               save_mean, save_invstd, workspace, st, stats, stats_rows);
+  return stem_fwd_impl<float>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, 1, y, argmax,
+                              save_mean, save_invstd, workspace, st, stats, stats_rows);
 }

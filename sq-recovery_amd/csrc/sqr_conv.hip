@@ -59,6 +59,7 @@ struct NTArgs {
   void* out;       // [M][Nout] (os == 1) or the strided pixel subset of an [N][oH][oW][Nout] tensor
   int os, oph, opw, oH, oW;  // out pixel of row (n,i,j) = (n, i*os+oph, j*os+opw)
   int ntm, ntn;    // tile counts
+  float* stats;    // nullable: per-M-tile BatchNorm partials [ntm][2][Nout] (sum, sum of squares)
 };
 
 struct TNArgs {
@@ -68,6 +69,7 @@ struct TNArgs {
   int kchunk;        // pixels per split
   float* slab;       // [splits][Kout][Ng]
   int ntm, ntn;
+  int rect_wt;       // > 0: every BK-pixel tile is a rect_wt-wide rectangle of one image (no divides)
 };
 
 template <typename T> struct Cfg;
@@ -316,6 +318,58 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
       if (m < g.M) store4(out + orow[i] * a.Nout + n, acc[j][i]);
     }
   }
+  if (a.stats) {
+    // fused BatchNorm statistics of the STORED (dtype-rounded) output: per channel sum and sum of
+    // squares over this M-tile -> stats[tile_m][0/1][n]; the BN layer finalizes from these
+    // partials instead of re-reading the whole activation.
+    float* red = (float*)smem;  // [WAVES_M][BN][2]; the k loop ended with a barrier
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WM + 16 * i + fr;
+        if (m < g.M) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v = (float)(T)acc[j][i][e];
+            s1[e] += v;
+            s2[e] = fmaf(v, v, s2[e]);
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          s1[e] += __shfl_xor(s1[e], off, 64);
+          s2[e] += __shfl_xor(s2[e], off, 64);
+        }
+      }
+      if (fr == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int col = wn * WN + 16 * j + 4 * fq + e;
+          red[(wm * BN + col) * 2] = s1[e];
+          red[(wm * BN + col) * 2 + 1] = s2[e];
+        }
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < BN; t += 256) {
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES_M; ++w) {
+        a1 += red[(w * BN + t) * 2];
+        a2 += red[(w * BN + t) * 2 + 1];
+      }
+      const int n = n0 + t;
+      if (n < a.Nout) {
+        a.stats[((size_t)tile_m * 2) * a.Nout + n] = a1;
+        a.stats[((size_t)tile_m * 2 + 1) * a.Nout + n] = a2;
+      }
+    }
+  }
 }
 
 // ============================================================================ TN (wgrad)
@@ -354,11 +408,42 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   const int p_begin = blockIdx.y * a.kchunk;
   const int p_end = min(p_begin + a.kchunk, g.M);
 
-  const T* __restrict__ dyb = (const T*)a.dy;
-  const T* __restrict__ xb = (const T*)g.base;
-  // per lane: row within its instruction and physical chunk
+  // Buffer-descriptor LDS-DMA loads (out-of-range voffset -> zeros).  Per (lane, instruction) the
+  // 16-B column chunk — hence the tap (r,s) and channel of the X gather — is fixed for the whole
+  // kernel; per tile only the pixel moves.  With rect_wt, a BK-pixel tile is a rect_wt-wide
+  // rectangle of one image, so a lane's pixel is the tile origin (scalar) + a per-lane constant.
+  constexpr uint32_t kOOB = 0x80000000u;
   const int qr = lane / QCPR, qc = lane % QCPR;
   const int pr = lane / PCPR, pc = lane % PCPR;
+  uint32_t q_col[QI];
+  int q_row[QI];
+#pragma unroll
+  for (int i = 0; i < QI; ++i) {
+    const int row = (i * 4 + wave) * QRPI + qr;
+    const int lch = 2 * tn_swz<QNW>(row, qc >> 1) + (qc & 1);
+    const int col = m0 + lch * C::VEC;
+    q_row[i] = row;
+    q_col[i] = col < a.Kout ? (uint32_t)(col * C::ES) : kOOB;
+  }
+  int p_row[PI], p_dh[PI], p_dw[PI], p_coff[PI], p_rr[PI], p_cc[PI];
+#pragma unroll
+  for (int i = 0; i < PI; ++i) {
+    const int row = (i * 4 + wave) * PRPI + pr;
+    const int lch = 2 * tn_swz<PNW>(row, pc >> 1) + (pc & 1);
+    const int col = n0 + lch * C::VEC;
+    const int tap = col >> g.log2Ci, c = col & (g.Ci - 1);
+    const int tr = (int)fdiv((uint32_t)tap, g.fd_s);
+    p_row[i] = row;
+    p_dh[i] = col < a.Ng ? g.off_h + tr * g.ks : -(1 << 28);  // invalid column fails the bounds test
+    p_dw[i] = g.off_w + (tap - tr * g.S) * g.ks;
+    p_coff[i] = c * C::ES;
+    p_rr[i] = a.rect_wt > 0 ? row / a.rect_wt : 0;
+    p_cc[i] = a.rect_wt > 0 ? row - p_rr[i] * a.rect_wt : 0;
+  }
+  const __amdgpu_buffer_rsrc_t qsrd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, (uint32_t)((size_t)g.M * a.Kout * C::ES), 0x00020000);
+  const __amdgpu_buffer_rsrc_t psrd = __builtin_amdgcn_make_buffer_rsrc((void*)g.base, 0, g.bytes, 0x00020000);
+  const int pixstride = g.Ci * C::ES;
 
   auto issue = [&](int kt, int stage) {
     char* q = smem + stage * STAGE;
@@ -366,32 +451,37 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
     const int pix0 = p_begin + kt * BK;
 #pragma unroll
     for (int i = 0; i < QI; ++i) {
-      const int row = (i * 4 + wave) * QRPI + qr;
-      const int lch = 2 * tn_swz<QNW>(row, qc >> 1) + (qc & 1);  // logical chunk
-      const int px = pix0 + row, col = m0 + lch * C::VEC;
-      const bool ok = px < p_end && col < a.Kout;
-      const void* src = ok ? (const void*)(dyb + ((size_t)px * a.Kout + col)) : (const void*)g_zero16;
-      glds16(src, q + (i * 4 + wave) * QRPI * QROWB);
+      const int px = pix0 + q_row[i];
+      const uint32_t voff = px < p_end ? (uint32_t)(px * a.Kout * C::ES) + q_col[i] : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qsrd, (__attribute__((address_space(3))) void*)(q + (i * 4 + wave) * QRPI * QROWB),
+                                               16, voff, 0, 0, 0);
+    }
+    int n0i = 0, oh0 = 0, ow0 = 0;
+    if (a.rect_wt > 0) {  // tile origin: wave-uniform
+      n0i = (int)fdiv((uint32_t)pix0, g.fd_hw);
+      const int rem = pix0 - n0i * g.Ho * g.Wo;
+      oh0 = (int)fdiv((uint32_t)rem, g.fd_w);
+      ow0 = rem - oh0 * g.Wo;
     }
 #pragma unroll
     for (int i = 0; i < PI; ++i) {
-      const int row = (i * 4 + wave) * PRPI + pr;
-      const int lch = 2 * tn_swz<PNW>(row, pc >> 1) + (pc & 1);
-      const int px = pix0 + row, col = n0 + lch * C::VEC;
-      bool ok = px < p_end && col < a.Ng;
-      const void* src = (const void*)g_zero16;
-      if (ok) {
-        const int tap = col >> g.log2Ci, c = col & (g.Ci - 1);
-        const int tr = (int)fdiv((uint32_t)tap, g.fd_s), ts = tap - tr * g.S;
-        const int n = (int)fdiv((uint32_t)px, g.fd_hw);
+      const int px = pix0 + p_row[i];
+      int n, oh, ow;
+      if (a.rect_wt > 0) {
+        n = n0i;
+        oh = oh0 + p_rr[i];
+        ow = ow0 + p_cc[i];
+      } else {
+        n = (int)fdiv((uint32_t)px, g.fd_hw);
         const int rem = px - n * g.Ho * g.Wo;
-        const int oh = (int)fdiv((uint32_t)rem, g.fd_w);
-        const int ow = rem - oh * g.Wo;
-        const int h = oh * g.ms + g.off_h + tr * g.ks, w = ow * g.ms + g.off_w + ts * g.ks;
-        if (h >= 0 && h < g.Hi && w >= 0 && w < g.Wi)
-          src = (const void*)(xb + ((size_t)((n * g.Hi + h) * g.Wi + w) * g.Ci + c));
+        oh = (int)fdiv((uint32_t)rem, g.fd_w);
+        ow = rem - oh * g.Wo;
       }
-      glds16(src, p + (i * 4 + wave) * PRPI * PROWB);
+      const int h = oh * g.ms + p_dh[i], w = ow * g.ms + p_dw[i];
+      const bool ok = px < p_end && (unsigned)h < (unsigned)g.Hi && (unsigned)w < (unsigned)g.Wi;
+      const uint32_t voff = ok ? (uint32_t)(((n * g.Hi + h) * g.Wi + w) * pixstride + p_coff[i]) : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(psrd, (__attribute__((address_space(3))) void*)(p + (i * 4 + wave) * PRPI * PROWB),
+                                               16, voff, 0, 0, 0);
     }
   };
 
@@ -769,16 +859,19 @@ Gather make_gather(const void* base, int Hi, int Wi, int Ci, int Ho, int Wo, int
   return g;
 }
 
+int nt_cfg(int M, int N) {
+  auto nblk = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (N >= 128 && nblk(128, 128) >= 512) return 0;
+  if (nblk(128, 64) >= 512) return 1;
+  if (N >= 128 && nblk(64, 128) >= 512) return 2;
+  return 3;
+}
+
 template <typename T>
 int launch_nt(NTArgs a, hipStream_t st) {
   // tile choice: biggest tile that still gives >= 2 workgroups per CU (512), else the smallest
   const int M = a.g.M, N = a.Nout;
-  auto nblk = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  int cfg;
-  if (N >= 128 && nblk(128, 128) >= 512) cfg = 0;
-  else if (nblk(128, 64) >= 512) cfg = 1;
-  else if (N >= 128 && nblk(64, 128) >= 512) cfg = 2;
-  else cfg = 3;
+  const int cfg = nt_cfg(M, N);
   int bm = (cfg == 0 || cfg == 1) ? 128 : 64, bn = (cfg == 0 || cfg == 2) ? 128 : 64;
   a.ntm = (M + bm - 1) / bm;
   a.ntn = (N + bn - 1) / bn;
@@ -885,8 +978,8 @@ static int im2col(const void* x, const sqr_conv_desc* d, const Shape& sh, void* 
   return 0;
 }
 
-extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d,
-                              void* workspace, size_t workspace_bytes, void* stream) {
+static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
+                         int* stats_rows, void* workspace, size_t workspace_bytes, void* stream) {
   Shape sh;
   int rc = check_desc(d, &sh);
   if (rc) return rc;
@@ -900,6 +993,8 @@ extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const 
   a.oph = a.opw = 0;
   a.oH = sh.Ho;
   a.oW = sh.Wo;
+  a.stats = stats;
+  if (stats_rows) *stats_rows = (sh.M + ((nt_cfg(sh.M, d->K) <= 1) ? 128 : 64) - 1) / ((nt_cfg(sh.M, d->K) <= 1) ? 128 : 64);
   if (sh.im2col) {
     const size_t need = sqr_conv2d_workspace_bytes(d, 0);
     if (workspace_bytes < need || !workspace) {
@@ -915,6 +1010,23 @@ extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const 
     a.Kg = d->R * d->S * d->C;
   }
   return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
+}
+
+extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  return conv_fwd_impl(x, w_krsc, y, d, nullptr, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d) {
+  Shape sh;
+  if (check_desc(d, &sh)) return 0;
+  return (size_t)((sh.M + 63) / 64) * 2 * d->K;
+}
+
+extern "C" int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
+                                    int* stats_rows, void* workspace, size_t workspace_bytes, void* stream) {
+  SQR_CHECK_ARG(stats && stats_rows, "conv2d_fwd_stats: null stats output");
+  return conv_fwd_impl(x, w_krsc, y, d, stats, stats_rows, workspace, workspace_bytes, stream);
 }
 
 // dgrad parity class (ph, pw) of a stride-st conv: taps r = r0 + st*t with (ph + pad - r) % st == 0
@@ -961,6 +1073,7 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
       a.Kg = c.Rc * c.Sc * d->K;  // 0 -> the class receives no gradient: zeros are written
       a.out = dx;
       a.os = d->stride;
+      a.stats = nullptr;
       a.oph = ph;
       a.opw = pw;
       a.oH = d->H;
@@ -1008,6 +1121,12 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   a.Kout = d->K;
   a.Ng = Ng;
   a.slab = (float*)ws;
+  {
+    const int BK = 128 / sh.ES, Wo = a.g.Wo, Ho = a.g.Ho;
+    a.rect_wt = 0;
+    if (Wo % BK == 0) a.rect_wt = BK;
+    else if (BK % Wo == 0 && Ho % (BK / Wo) == 0) a.rect_wt = Wo;
+  }
   const TNPlan p = plan_tn(d->K, Ng, sh.M, sh.ES);
   rc = d->dtype == SQR_DTYPE_BF16 ? launch_tn<bf16>(a, p, st) : launch_tn<float>(a, p, st);
   if (rc) return rc;

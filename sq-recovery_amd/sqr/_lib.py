@@ -46,6 +46,9 @@ SIGNATURES = {
     "sqr_conv2d_pack_weights": (c_int, [ctypes.POINTER(SqrPackJob), c_int, c_void_p]),
     "sqr_conv2d_fwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t,
                                c_void_p]),
+    "sqr_conv2d_stats_floats": (c_size_t, [ctypes.POINTER(SqrConvDesc)]),
+    "sqr_conv2d_fwd_stats": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
+                                     ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                     c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
@@ -58,6 +61,12 @@ SIGNATURES = {
                            c_size_t, c_void_p]),
     "sqr_bn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_bn_fwd_stats": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_float, c_float, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_size_t, c_void_p]),
+    "sqr_stem_fwd_stats": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_size_t, c_void_p]),
     "sqr_stem_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "sqr_stem_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,

@@ -35,7 +35,7 @@ def _ws_bytes(M, C):
 
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps):
+    def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps, stats=None):
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
@@ -47,11 +47,18 @@ class BNActFn(torch.autograd.Function):
         invstd = torch.empty(C, **f32)
         n = _ws_bytes(M, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(lib().sqr_bn_fwd(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(bias),
-                               ptr(rmean) if rmean is not None else ctypes.c_void_p(0),
-                               ptr(rvar) if rvar is not None else ctypes.c_void_p(0),
-                               ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(residual), int(relu),
-                               ptr(y), ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_bn_fwd")
+        rm = ptr(rmean) if rmean is not None else ctypes.c_void_p(0)
+        rv = ptr(rvar) if rvar is not None else ctypes.c_void_p(0)
+        if training and stats is not None:  # batch statistics from the producing conv's epilogue
+            check(lib().sqr_bn_fwd_stats(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(stats), stats.shape[0],
+                                         ptr(weight), ptr(bias), rm, rv, ctypes.c_float(momentum),
+                                         ctypes.c_float(eps), ptr(residual), int(relu), ptr(y), ptr(mean),
+                                         ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_bn_fwd_stats")
+        else:
+            check(lib().sqr_bn_fwd(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(bias), rm, rv,
+                                   ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(residual),
+                                   int(relu), ptr(y), ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)),
+                  "sqr_bn_fwd")
         ctx.relu, ctx.training, ctx.eps = relu, training, eps
         ctx.has_res = residual is not None
         if training:
@@ -72,7 +79,7 @@ class BNActFn(torch.autograd.Function):
             xhat = (x.float() - m.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
             dx = (g * (weight * invstd).view(1, C, 1, 1)).to(x.dtype)
             dres = g.to(x.dtype) if ctx.has_res else None
-            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None
+            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
@@ -84,7 +91,7 @@ class BNActFn(torch.autograd.Function):
                                stream_ptr(x.device)), "sqr_bn_bwd")
         if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
             dres = dy
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None
 
 
 def count_batches(bns):
@@ -95,22 +102,41 @@ def count_batches(bns):
         torch._foreach_add_(t, 1)
 
 
+def _split(x):
+    # x may be a conv's (y, partials) pair (sqr.conv.conv2d(stats=True))
+    if isinstance(x, tuple):
+        return x
+    return x, None
+
+
+def _check_stats(stats, x):
+    if stats is not None:
+        C = x.shape[1]
+        if stats.dtype != torch.float32 or stats.dim() != 3 or stats.shape[1:] != (2, C) or not stats.is_contiguous():
+            raise ValueError("sqr bn: statistics partials must be f32 [rows, 2, C]")
+    return stats
+
+
 def bn_act(x, bn, residual=None, relu=True, counted=False):
-    """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics."""
+    """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics.
+    x may be a (y, partials) pair from a stats-producing conv: training mode then takes the batch
+    statistics from the partials instead of reducing over y."""
+    x, stats = _split(x)
     training = bn.training or not bn.track_running_stats
     if training and bn.track_running_stats and not counted:
         bn.num_batches_tracked.add_(1)
     mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps))
+    return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
+                         _check_stats(stats, x))
 
 
 class StemFn(torch.autograd.Function):
     """maxpool3x3/2/1(relu(bn(x))) — torchvision resnet stem after conv1."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, rmean, rvar, training, momentum, eps):
+    def forward(ctx, x, weight, bias, rmean, rvar, training, momentum, eps, stats=None):
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
@@ -121,11 +147,17 @@ class StemFn(torch.autograd.Function):
         invstd = torch.empty(C, **f32)
         n = lib().sqr_stem_workspace_bytes(N, H, W, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(lib().sqr_stem_fwd(ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(bias),
-                                 ptr(rmean) if rmean is not None else ctypes.c_void_p(0),
-                                 ptr(rvar) if rvar is not None else ctypes.c_void_p(0), ctypes.c_float(momentum),
-                                 ctypes.c_float(eps), int(training), ptr(y), ptr(arg), ptr(mean), ptr(invstd), ptr(ws),
-                                 n, stream_ptr(x.device)), "sqr_stem_fwd")
+        rm = ptr(rmean) if rmean is not None else ctypes.c_void_p(0)
+        rv = ptr(rvar) if rvar is not None else ctypes.c_void_p(0)
+        if training and stats is not None:
+            check(lib().sqr_stem_fwd_stats(ptr(x), N, H, W, C, _dt(x), ptr(stats), stats.shape[0], ptr(weight),
+                                           ptr(bias), rm, rv, ctypes.c_float(momentum), ctypes.c_float(eps), ptr(y),
+                                           ptr(arg), ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)),
+                  "sqr_stem_fwd_stats")
+        else:
+            check(lib().sqr_stem_fwd(ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(bias), rm, rv,
+                                     ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(y), ptr(arg),
+                                     ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_stem_fwd")
         if not training:
             ctx.mark_non_differentiable(y)
         ctx.save_for_backward(x, y, arg, weight, mean, invstd)
@@ -146,14 +178,15 @@ class StemFn(torch.autograd.Function):
         check(lib().sqr_stem_bwd(ptr(dy), ptr(y), ptr(arg), ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(mean),
                                  ptr(invstd), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n, stream_ptr(x.device)),
               "sqr_stem_bwd")
-        return dx, dgamma, dbeta, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, None, None, None, None
 
 
 def stem(x, bn, counted=False):
+    x, stats = _split(x)
     training = bn.training or not bn.track_running_stats
     if training and bn.track_running_stats and not counted:
         bn.num_batches_tracked.add_(1)
     mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    return StemFn.apply(x, bn.weight, bn.bias, rm, rv, bool(training), mom, float(bn.eps))
+    return StemFn.apply(x, bn.weight, bn.bias, rm, rv, bool(training), mom, float(bn.eps), _check_stats(stats, x))

@@ -126,16 +126,31 @@ def clear_packed(convs):
         m._packed = None
 
 
-def conv2d_fwd(x, w_krsc, d, return_ws=False):
-    """y = conv(x); with return_ws the workspace (holding the im2col matrix for C<8) is returned too."""
+def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
+    """y = conv(x); with return_ws the workspace (holding the im2col matrix for C<8) is returned
+    too; with stats the BatchNorm partials [rows, 2, K] (f32 per-tile sum / sum of squares of y,
+    see sqr_conv2d_fwd_stats) are returned after y."""
     import ctypes
     ho, wo = _out_hw(d)
     dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
     y = torch.empty((d.N, d.K, ho, wo), dtype=dt, device=x.device, memory_format=_CL)
     ws, n = _ws(d, 0, x.device)
+    st = None
     with _Probe("fwd", d):
-        rc = lib().sqr_conv2d_fwd(ptr(x), ptr(w_krsc), ptr(y), ctypes.byref(d), ptr(ws), n, stream_ptr(x.device))
+        if stats:
+            L = lib()
+            nf = L.sqr_conv2d_stats_floats(ctypes.byref(d))
+            st = torch.empty(nf, dtype=torch.float32, device=x.device)
+            rows = ctypes.c_int()
+            rc = L.sqr_conv2d_fwd_stats(ptr(x), ptr(w_krsc), ptr(y), ctypes.byref(d), ptr(st), ctypes.byref(rows),
+                                        ptr(ws), n, stream_ptr(x.device))
+        else:
+            rc = lib().sqr_conv2d_fwd(ptr(x), ptr(w_krsc), ptr(y), ctypes.byref(d), ptr(ws), n,
+                                      stream_ptr(x.device))
     check(rc, "sqr_conv2d_fwd")
+    if stats:
+        st = st[:rows.value * 2 * d.K].view(rows.value, 2, d.K)
+        return (y, st, ws) if return_ws else (y, st)
     return (y, ws) if return_ws else y
 
 
@@ -181,7 +196,7 @@ def compute_dtype(x):
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, dt, packed):
+    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False):
         N, C, H, W = x.shape
         K, _, R, S = weight.shape
         xin = x.to(dt).contiguous(memory_format=_CL)
@@ -191,7 +206,11 @@ class Conv2dFn(torch.autograd.Function):
             krsc, crsk = packed
         else:
             krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
-        y, ws = conv2d_fwd(xin, krsc, d, return_ws=True)
+        stats = None
+        if want_stats and bias is None:
+            y, stats, ws = conv2d_fwd(xin, krsc, d, return_ws=True, stats=True)
+        else:
+            y, ws = conv2d_fwd(xin, krsc, d, return_ws=True)
         if bias is not None:
             y = y + bias.to(dt).view(1, K, 1, 1)
         ctx.d = d
@@ -200,10 +219,14 @@ class Conv2dFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1]
         col = ws if (need_w and C < 8) else None  # im2col matrix, reused by the weight gradient
         ctx.save_for_backward(xin if (need_w and col is None) else None, crsk, col)
+        if want_stats:
+            if stats is not None:
+                ctx.mark_non_differentiable(stats)
+            return y, stats
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, *_):
         xin, crsk, col = ctx.saved_tensors
         d = ctx.d
         dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
@@ -217,13 +240,16 @@ class Conv2dFn(torch.autograd.Function):
             dw = conv2d_bwd_weight(xin, g, d, col)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None):
+def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False):
+    """conv(x); with stats=True returns (y, partials) where partials feed the following
+    BatchNorm (sqr.bn.bn_act / stem ``stats=``) so it skips its statistics pass over y
+    (partials is None when the conv has a bias)."""
     if not x.is_cuda:
         raise ValueError("sqr conv2d runs on MI355X; got a %s tensor" % x.device)
-    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed)
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed, bool(stats))
 
 
 class Conv2d(nn.Conv2d):
@@ -238,11 +264,20 @@ class Conv2d(nn.Conv2d):
             raise ValueError("sqr Conv2d supports groups=1, dilation=1, symmetric stride/padding only")
         self._packed = None  # ((weight version, dtype, ptr), krsc, crsk, fp32 source) from pack_all
 
-    def forward(self, x):
+    def _cached(self, x):
         dt = compute_dtype(x) if x.is_cuda else None
-        packed = None
         if self._packed is not None and dt is not None:
             key, krsc, crsk, _ = self._packed
             if key == (self.weight._version, dt, self.weight.data_ptr()):
-                packed = (krsc, crsk)
-        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], packed)
+                return (krsc, crsk)
+        return None
+
+    def forward(self, x):
+        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x))
+
+    def forward_stats(self, x, bn=None):
+        """(y, BatchNorm partials of y) — see conv2d(stats=True).  With `bn` given, the partials
+        are produced only when that BatchNorm will use batch statistics (else y alone)."""
+        if bn is not None and not (bn.training or not bn.track_running_stats):
+            return self.forward(x)
+        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x), stats=True)

@@ -31,11 +31,13 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         # conv -> fused [bn+relu] -> conv -> fused [bn + identity + relu]   (libsqr kernels)
-        out = bn_act(self.conv1(x), self.bn1, relu=True, counted=True)
+        # (training: each conv's epilogue also emits the batch statistics its BN needs)
+        out = bn_act(self.conv1.forward_stats(x, self.bn1), self.bn1, relu=True, counted=True)
         identity = x
         if self.downsample is not None:
-            identity = bn_act(self.downsample[0](x), self.downsample[1], relu=False, counted=True)
-        return bn_act(self.conv2(out), self.bn2, residual=identity, relu=True, counted=True)
+            identity = bn_act(self.downsample[0].forward_stats(x, self.downsample[1]),
+                              self.downsample[1], relu=False, counted=True)
+        return bn_act(self.conv2.forward_stats(out, self.bn2), self.bn2, residual=identity, relu=True, counted=True)
 
 
 class ResNet18(nn.Module):
@@ -76,7 +78,7 @@ class ResNet18(nn.Module):
             pack_all(convs, compute_dtype(x))
         count_batches([m for m in self.modules() if isinstance(m, nn.BatchNorm2d)])
         try:
-            x = stem(self.conv1(x), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
+            x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             clear_packed(convs)  # packed weights live on in autograd's saved tensors only

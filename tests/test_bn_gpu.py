@@ -111,3 +111,51 @@ def test_stem_eval_matches_torch():
     with torch.no_grad():
         y = stem(x.to(DEV).contiguous(memory_format=torch.channels_last), bn.to(DEV))
     assert _rel(y, ref) <= 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("cfg", [(2, 64, 64, 15, 3, 1), (3, 64, 128, 9, 3, 2), (2, 128, 256, 7, 1, 2),
+                                 (1, 256, 512, 5, 3, 1), (4, 32, 64, 33, 3, 1)],
+                         ids=lambda c: "N%dC%dK%dH%dR%ds%d" % c)
+def test_conv_bn_stats_fused(cfg, dtype):
+    """BN batch statistics taken from the conv epilogue partials (sqr_conv2d_fwd_stats ->
+    sqr_bn_fwd_stats) == statistics reduced over the stored conv output (sqr_bn_fwd)."""
+    from sqr.bn import bn_act
+    from sqr.conv import conv2d
+    N, C, K, H, R, s = cfg
+    g = torch.Generator().manual_seed(N * C + H)
+    x = torch.randn(N, C, H, H, generator=g).to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, generator=g) * 0.1 + 0.02).to(DEV)
+    bn_a, bn_b = _bn(K, 5).to(DEV).train(), _bn(K, 5).to(DEV).train()
+    with torch.no_grad():
+        y, st = conv2d(x, w, None, s, R // 2, stats=True)
+        y2 = conv2d(x, w, None, s, R // 2)
+        assert torch.equal(y, y2)
+        Ho = y.shape[2]
+        assert st.shape[1:] == (2, K) and st.shape[0] * 64 >= N * Ho * Ho
+        yf = y.double()
+        ref_sum = yf.sum((0, 2, 3))
+        assert _rel(st.double().sum(0)[0], ref_sum) <= 1e-5
+        assert _rel(st.double().sum(0)[1], (yf * yf).sum((0, 2, 3))) <= 1e-5
+        a = bn_act((y, st), bn_a, relu=True)
+        b = bn_act(y, bn_b, relu=True)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(a, b) <= tol
+    assert _rel(bn_a.running_mean, bn_b.running_mean) <= 1e-5
+    assert _rel(bn_a.running_var, bn_b.running_var) <= 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_stem_stats_fused(dtype):
+    from sqr.bn import stem
+    from sqr.conv import conv2d
+    g = torch.Generator().manual_seed(9)
+    x = torch.rand(2, 1, 70, 70, generator=g).to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 1, 7, 7, generator=g) * 0.2).to(DEV)
+    bn_a, bn_b = _bn(64, 6).to(DEV).train(), _bn(64, 6).to(DEV).train()
+    with torch.no_grad():
+        y, st = conv2d(x, w, None, 2, 3, stats=True)
+        a = stem((y, st), bn_a)
+        b = stem(y, bn_b)
+    assert _rel(a, b) <= (1e-5 if dtype == torch.float32 else 1e-2)
+    assert _rel(bn_a.running_var, bn_b.running_var) <= 1e-5
