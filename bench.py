@@ -34,16 +34,6 @@ PEAK_HBM_GBS = 8000.0
 PROBE = ("wgrad", 64, 64, 3, 1)  # phase, C, H(=W), R, stride  (N = per-GPU batch)
 
 
-def synth_params(rng, n):
-    a = rng.uniform(25, 75, (n, 3)) / 255.0
-    e = rng.uniform(0.1, 1.0, (n, 2))
-    t = (128.0 + rng.uniform(-40, 40, (n, 3))) / 255.0
-    u = rng.uniform(0, 1, (n, 3))
-    q = np.stack([np.sqrt(1 - u[:, 0]) * np.sin(2 * np.pi * u[:, 1]), np.sqrt(1 - u[:, 0]) * np.cos(2 * np.pi * u[:, 1]),
-                  np.sqrt(u[:, 0]) * np.sin(2 * np.pi * u[:, 2]), np.sqrt(u[:, 0]) * np.cos(2 * np.pi * u[:, 2])], 1)
-    return np.concatenate([a, e, t, q], 1).astype(np.float32)
-
-
 def conv_flops(N, C, H, K, R, stride):
     pad = R // 2
     Ho = (H + 2 * pad - R) // stride + 1
@@ -88,14 +78,8 @@ def main():
                     help="capture the whole train step in a HIP graph (1/0; default: on for 1 GPU)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    from sqr import dist
+    rank, world, dev = dist.init("nccl")
 
     import classes
     import models
@@ -104,17 +88,13 @@ def main():
 
     B, R, H = args.batch, args.render, 256
     rng = np.random.default_rng(1234 + rank)
-    params = torch.tensor(synth_params(rng, B), device=dev)
+    params = torch.tensor(classes.sample_sq_params(rng, B), device=dev)
     images = losses.implicit_render(params, H, 1.5, 260).unsqueeze(1).contiguous()  # [B,1,256,256] in [0,1]
 
     torch.manual_seed(0)  # identical init on every rank (DDP also broadcasts)
     net = models.ResNetSQ(outputs=4, pretrained=False).to(dev)
     state0 = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
-    model = net
-    if world > 1:
-        from torch.nn.parallel import DistributedDataParallel as DDP
-        model = DDP(net, device_ids=[local], bucket_cap_mb=16, gradient_as_bucket_view=True,
-                    broadcast_buffers=False)
+    model = dist.wrap(net, dev)  # DDP (RCCL all-reduce overlapped with backward) when world > 1
     use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
     opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0, fused=True, capturable=use_graph)
     crit = classes.ImplicitLoss(R, dev, 1.5, 260)
@@ -153,8 +133,7 @@ def main():
         step = graph_step
 
     def barrier():
-        if world > 1:
-            torch.distributed.barrier()
+        dist.barrier()
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -181,10 +160,7 @@ def main():
     events = sconv.probe_events()
     sconv.set_probe(None, 0, 0, 0, 0, 0, 0)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = t.item()
+    dt = dist.max_over_ranks(dt)
     mean_loss = (loss_acc / args.steps).item()
 
     if args.breakdown and rank == 0:
@@ -231,8 +207,7 @@ def main():
                                          % (args.cpu_steps, B, R, secs)}
     if rank == 0:
         print(json.dumps(out))
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    dist.finish()
 
 
 if __name__ == "__main__":

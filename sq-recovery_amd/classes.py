@@ -101,6 +101,54 @@ class H5Dataset(data.Dataset):
         return self.labels[ID][:12]
 
 
+def sample_sq_params(rng, n):
+    """Random SQ labels in the reference's normalised layout [a/255 (3), e (2), t/255 (3), q (4)]
+    drawn from its generator distribution (gen_rand_rot.py:21-31, test_random.py:34-37,
+    quaternion randquat helpers.py:286-292)."""
+    a = rng.uniform(25, 75, (n, 3)) / 255.0
+    e = rng.uniform(0.1, 1.0, (n, 2))
+    t = (128.0 + rng.uniform(-40, 40, (n, 3))) / 255.0
+    u = rng.uniform(0, 1, (n, 3))
+    q = np.stack([np.sqrt(1 - u[:, 0]) * np.sin(2 * np.pi * u[:, 1]), np.sqrt(1 - u[:, 0]) * np.cos(2 * np.pi * u[:, 1]),
+                  np.sqrt(u[:, 0]) * np.sin(2 * np.pi * u[:, 2]), np.sqrt(u[:, 0]) * np.cos(2 * np.pi * u[:, 2])], 1)
+    return np.concatenate([a, e, t, q], 1).astype(np.float32)
+
+
+class SyntheticDataset(data.Dataset):
+    """H5Dataset stand-in without files: n random SQs (sample_sq_params) rendered on the GPU into
+    size x size depth images in [0, 1] with the implicit-loss renderer (tau 1.5, sharpness 260),
+    held in HBM.  Same interface (set_mode / __len__ / __getitem__ -> (X [1,H,W], y [12]));
+    items are device tensors, so use a DataLoader with num_workers=0 (or batches()).
+    Rank r of a data-parallel job passes seed + r to get its own shard."""
+
+    def __init__(self, n, device, train_split=0.9, size=256, seed=0, tau=1.5, sharpness=260):
+        rng = np.random.default_rng(seed)
+        self.labels = torch.tensor(sample_sq_params(rng, n), device=device)
+        self.images = torch.empty((n, 1, size, size), dtype=torch.float32, device=device)
+        for i in range(0, n, 256):  # bounded render batches
+            self.images[i:i + 256, 0] = _L.implicit_render(self.labels[i:i + 256], size, tau, sharpness)
+        self.n_train = int(train_split * n)
+        self.n_val = n - self.n_train
+        self.mode = 0
+
+    def set_mode(self, mode):
+        self.mode = mode
+
+    def __len__(self):
+        return self.n_train if self.mode == 0 else self.n_val
+
+    def __getitem__(self, index):
+        if self.mode == 1:
+            index += self.n_train
+        return self.images[index], self.labels[index]
+
+    def batches(self, batch_size):
+        """Contiguous device batches of the current split (no host round trip)."""
+        off = 0 if self.mode == 0 else self.n_train
+        for i in range(0, len(self) - batch_size + 1, batch_size):
+            yield self.images[off + i:off + i + batch_size], self.labels[off + i:off + i + batch_size]
+
+
 class QuaternionLoss:
     """classes.py:96-106: 1 - 2|0.5 - <q_pred,q_true>^2|."""
 

@@ -103,6 +103,27 @@ def compare_images(params_true, params_pred, wait=16):
         cv2.waitKey(wait)
 
 
+def read_image_gray(path):
+    """cv2.imread(path, 0) for the scanner's 24-bit BMPs without OpenCV (uses cv2 when present for
+    other formats).  Gray = the common channel value; genuinely colour BMPs use cv2's weights."""
+    with open(path, "rb") as f:
+        b = f.read()
+    if b[:2] != b"BM" or int.from_bytes(b[28:30], "little") != 24:
+        import cv2
+        return cv2.imread(path, 0)
+    off = int.from_bytes(b[10:14], "little")
+    w = int.from_bytes(b[18:22], "little", signed=True)
+    h = int.from_bytes(b[22:26], "little", signed=True)
+    stride = (w * 3 + 3) & ~3
+    rows = np.frombuffer(b[off:off + stride * abs(h)], np.uint8).reshape(abs(h), stride)[:, :w * 3]
+    bgr = rows.reshape(abs(h), w, 3)
+    if (bgr[..., 0] == bgr[..., 1]).all() and (bgr[..., 1] == bgr[..., 2]).all():
+        img = bgr[..., 0]
+    else:
+        img = np.clip(np.rint(0.114 * bgr[..., 0] + 0.587 * bgr[..., 1] + 0.299 * bgr[..., 2]), 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(img[::-1] if h > 0 else img)
+
+
 def change_lr(opt, lr):
     for g in opt.param_groups:
         g["lr"] = lr

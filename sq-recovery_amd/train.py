@@ -1,0 +1,168 @@
+"""Drop-in for torch/train.py (timoblak/sq-recovery) on MI355X.
+
+Same loop as the reference (train.py:72-175): per batch zero_grad -> ResNetSQ forward ->
+cat(a, e, t, q) -> ImplicitLoss(R, tau 1.5, s 260)(images, pred) -> backward -> Adam(1e-4) step ->
+loss.item(); NaN check on encoder.fc[0].weight.grad; per epoch a validation pass with the loss and
+IoUAccuracy(64, full=True), ReduceLROnPlateau(patience 25) on the validation loss, checkpoint
+(helpers.save_model format) whenever the validation loss improves.
+
+MI355X-specific:
+  * convs / BatchNorm / losses run on the libsqr HIP kernels (no CPU fallback);
+  * --bf16 runs the network under bf16 autocast (the loss kernel always consumes fp32 params);
+  * data parallel: launch with `torchrun --nproc-per-node 8 train.py ...` — one process per GPU,
+    DDP gradient all-reduce over RCCL, each rank trains on its own contiguous shard
+    (sqr.dist.shard), rank 0 logs and writes checkpoints (un-prefixed state-dict keys);
+  * --synthetic N trains on N GPU-rendered SQ images (no dataset files needed); otherwise the
+    reference's H5Dataset(dataset_location, parse_csv(labels), 0.9) is used (needs h5py).
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.optim as optim
+import torch.utils.data as data
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from classes import H5Dataset, ImplicitLoss, IoUAccuracy, SyntheticDataset  # noqa: E402
+from helpers import load_model, parse_csv, save_compare_images, save_model  # noqa: E402
+from models import ResNetSQ  # noqa: E402
+from sqr import dist  # noqa: E402
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--dataset-location", default="../data/data/")
+    ap.add_argument("--labels", default="../data/annotations/data_labels.csv")
+    ap.add_argument("--synthetic", type=int, default=0, help="train on N synthetic images instead of the h5 set")
+    ap.add_argument("--model-location", default="trained_models/model_full.pt")
+    ap.add_argument("--epochs", type=int, default=20000)
+    ap.add_argument("--batch-size", type=int, default=32, help="per-GPU batch")
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--render-size", type=int, default=64)
+    ap.add_argument("--log-interval", type=int, default=1)
+    ap.add_argument("--running-mean", type=int, default=100)
+    ap.add_argument("--pretrained", type=int, default=1)
+    ap.add_argument("--continue-training", action="store_true")
+    ap.add_argument("--bf16", action="store_true", help="bf16 autocast for the network")
+    ap.add_argument("--compare-images", action="store_true",
+                    help="render val batch 0 with the external scanner (helpers.save_compare_images)")
+    ap.add_argument("--max-steps", type=int, default=0, help="stop an epoch after this many steps (0 = all)")
+    return ap.parse_args(argv)
+
+
+def _batches(dataset, rank, world, batch_size):
+    """This rank's batches of the current split (contiguous shard, no shuffle, like the reference)."""
+    idx = dist.shard(len(dataset), rank, world)
+    if isinstance(dataset, SyntheticDataset):
+        off = 0 if dataset.mode == 0 else dataset.n_train
+        for i in range(idx.start, idx.stop - batch_size + 1, batch_size):
+            yield (dataset.images[off + i:off + i + batch_size], dataset.labels[off + i:off + i + batch_size])
+        return
+    loader = data.DataLoader(data.Subset(dataset, list(idx)), batch_size=batch_size, shuffle=False, num_workers=4)
+    yield from loader
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    rank, world, device = dist.init("nccl")
+    main_rank = rank == 0
+    if main_rank:
+        print("Using device: %s (world size %d)" % (device, world))
+
+    if args.synthetic:
+        # every rank renders the same set and trains on its own shard
+        dataset = SyntheticDataset(args.synthetic, device, train_split=0.9, seed=0)
+    else:
+        dataset = H5Dataset(args.dataset_location, parse_csv(args.labels), train_split=0.9, dataset_file="dataset.h5")
+
+    net = ResNetSQ(outputs=4, pretrained=bool(args.pretrained)).to(device)
+    optimizer = optim.Adam(net.parameters(), lr=args.lr, weight_decay=0)
+    scheduler = optim.lr_scheduler.ReduceLROnPlateau(optimizer, patience=25)
+    starting_epoch = 0
+    if args.continue_training:
+        if main_rank:
+            print("Continuing with training...")
+        starting_epoch, net, optimizer, _ = load_model(args.model_location, net, optimizer)
+    model = dist.wrap(net, device)
+
+    loss_criterion = ImplicitLoss(args.render_size, device, 1.5, 260)
+    accuracy_estimator = IoUAccuracy(render_size=64, device=device, full=True)
+
+    def forward(x):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.bf16):
+            out = model(x)
+        return torch.cat([o.float() for o in out], dim=1)
+
+    best_val_loss = None
+    mean_losses, mean_val_losses, mean_val_accs = [], [], []
+    for epoch in range(starting_epoch, args.epochs):
+        losses, val_losses, val_accuracies = [], [], []
+        net.train()
+        dataset.set_mode(0)
+        n_items = len(dataset)
+        for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size)):
+            if args.max_steps and batch_idx >= args.max_steps:
+                break
+            x, true_labels = x.to(device, non_blocking=True), true_labels.to(device, non_blocking=True)
+            optimizer.zero_grad()
+            pred_labels = forward(x)
+            loss = loss_criterion(x, pred_labels)
+            loss.backward()
+            optimizer.step()
+            losses.append(loss.item())
+            if torch.any(torch.isnan(net.encoder.fc[0].weight.grad)):
+                print("--------------- NAN GRADS!!!! ---------------")
+            if main_rank and batch_idx % args.log_interval == 0:
+                sys.stdout.write("\033[K")
+                print("Train Epoch: {} Step: {} [{}/{}]\tLoss: {:,.6f}".format(
+                    epoch, batch_idx, (batch_idx + 1) * len(x) * world, n_items,
+                    np.mean(losses[-args.running_mean:])), end="\r")
+        train_mean = dist.mean_over_ranks(np.mean(losses)) if losses else float("nan")
+        mean_losses.append(train_mean)
+        if main_rank:
+            sys.stdout.write("\033[K")
+            print("-" * 72)
+            print("Train Epoch: {} [(100%)]\tLoss: {:.6f}".format(epoch, train_mean))
+
+        net.eval()
+        dataset.set_mode(1)
+        with torch.no_grad():
+            for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size)):
+                if args.max_steps and batch_idx >= args.max_steps:
+                    break
+                x, true_labels = x.to(device), true_labels.to(device)
+                pred_labels = forward(x)
+                loss = loss_criterion(x, pred_labels)
+                acc = accuracy_estimator(true_labels, pred_labels)
+                if batch_idx == 0 and main_rank and args.compare_images:
+                    save_compare_images(true_labels.cpu().numpy(), pred_labels.cpu().numpy())
+                val_losses.append(loss.item())
+                val_accuracies.append(acc.item())
+        val_loss_mean = dist.mean_over_ranks(np.mean(val_losses)) if val_losses else float("nan")
+        val_accuracy_mean = dist.mean_over_ranks(np.mean(val_accuracies)) if val_accuracies else float("nan")
+        mean_val_accs.append(val_accuracies)
+        mean_val_losses.append(val_loss_mean)
+        scheduler.step(val_loss_mean)
+
+        if main_rank:
+            if best_val_loss is None or val_loss_mean < best_val_loss:
+                print("Saving first model.." if best_val_loss is None else "New best loss achieved. Saving model..")
+                best_val_loss = val_loss_mean
+                os.makedirs(os.path.dirname(args.model_location) or ".", exist_ok=True)
+                save_model(args.model_location, epoch, model, optimizer,
+                           {"loss": mean_losses, "val_loss": mean_val_losses, "val_acc": mean_val_accs})
+            print("-" * 72)
+            print("Validation Epoch: {}\tLoss: {:,.6f}\tAccuracy: {:,.6f}".format(epoch, val_loss_mean,
+                                                                                 val_accuracy_mean))
+            print("=" * 72)
+        else:
+            best_val_loss = val_loss_mean if best_val_loss is None else min(best_val_loss, val_loss_mean)
+    dist.finish()
+    return mean_losses, mean_val_losses
+
+
+if __name__ == "__main__":
+    main()

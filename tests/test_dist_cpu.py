@@ -1,0 +1,128 @@
+"""Data-parallel path on CPU with the gloo backend, world_size 2.
+
+* sqr.dist.shard: equal, disjoint, contiguous shards;
+* sqr.dist.max_over_ranks / mean_over_ranks (bench.py timing, train.py logging);
+* a DDP step wrapped exactly as bench.py / train.py wrap it (sqr.dist.wrap: bucket_cap_mb,
+  gradient_as_bucket_view, no buffer broadcast) equals the average of the per-rank independent
+  gradients — the documented N-GPU semantics (per-rank BatchNorm statistics) — checked on the
+  oracle's CPU ResNetSQ (the HIP model needs a GPU; the DDP wiring is model-agnostic);
+* helpers.save_model on the DDP-wrapped model writes un-prefixed keys that load into a bare model.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _paths():
+    for p in (os.path.join(ROOT, "sq-recovery_amd"), os.path.join(ROOT, "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _worker(rank, world, port, tmpdir, q):
+    try:
+        _paths()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        torch.set_num_threads(2)
+        from sqr import dist as sd
+        import ref_torch
+        import helpers
+        r, w, dev = sd.init("gloo")
+        assert (r, w, dev.type) == (rank, world, "cpu")
+        res = {}
+        res["max"] = sd.max_over_ranks(float(rank + 1))
+        res["mean"] = sd.mean_over_ranks(float(rank + 1))
+        res["shard"] = list(sd.shard(10, rank, world))
+
+        torch.manual_seed(0)
+        net = ref_torch.ResNetSQRef()
+        ref = ref_torch.ResNetSQRef()
+        ref.load_state_dict(net.state_dict())
+        model = sd.wrap(net, dev)
+        assert model is not net
+        g = torch.Generator().manual_seed(11)
+        batches = [torch.rand(2, 1, 64, 64, generator=g) for _ in range(world)]
+
+        def loss_of(m, x):
+            a, e, t, q = m(x)
+            return (torch.cat([a, e, t, q], 1) ** 2).mean()
+
+        loss_of(model, batches[rank]).backward()
+        # average of independent per-rank gradients
+        avg = None
+        for x in batches:
+            ref.zero_grad()
+            loss_of(ref, x).backward()
+            gr = [p.grad.clone() for p in ref.parameters()]
+            avg = gr if avg is None else [a + b for a, b in zip(avg, gr)]
+        avg = [a / world for a in avg]
+        err = max(((p.grad - a).abs().max() / a.abs().max().clamp_min(1e-30)).item()
+                  for p, a in zip(net.parameters(), avg))
+        res["grad_rel_err"] = err
+        if rank == 0:
+            path = os.path.join(tmpdir, "ck.pt")
+            opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+            helpers.save_model(path, 3, model, opt, {"loss": [1.0]})
+            ck = torch.load(path, weights_only=True)
+            res["keys_prefixed"] = any(k.startswith("module.") for k in ck["model_state_dict"])
+            fresh = ref_torch.ResNetSQRef()
+            fresh.load_state_dict(ck["model_state_dict"])
+            res["epoch"] = ck["epoch"]
+        sd.barrier()
+        sd.finish()
+        q.put((rank, res))
+    except Exception as e:  # surface worker failures in the parent
+        import traceback
+        q.put((rank, {"error": traceback.format_exc() + repr(e)}))
+
+
+def test_shard_single_process():
+    _paths()
+    from sqr import dist as sd
+    assert list(sd.shard(10, 0, 1)) == list(range(10))
+    parts = [list(sd.shard(11, r, 4)) for r in range(4)]
+    assert all(len(p) == 2 for p in parts)
+    flat = sum(parts, [])
+    assert len(set(flat)) == len(flat)
+    assert sd.max_over_ranks(3.5) == 3.5  # no process group: identity
+
+
+@pytest.mark.timeout(300)
+def test_ddp_gloo_world2(tmp_path):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, res = q.get(timeout=280)
+        out[r] = res
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+    assert out[0]["max"] == out[1]["max"] == 2.0
+    assert out[0]["mean"] == out[1]["mean"] == 1.5
+    assert out[0]["shard"] == [0, 1, 2, 3, 4] and out[1]["shard"] == [5, 6, 7, 8, 9]
+    for r in range(world):
+        assert out[r]["grad_rel_err"] < 1e-5, out[r]["grad_rel_err"]
+    assert out[0]["keys_prefixed"] is False and out[0]["epoch"] == 3
