@@ -375,9 +375,13 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
 // ============================================================================ TN (wgrad)
 // LDS tiles [BK pixels][cols]; 32-byte windows XOR-swizzled by row so that the transposing
 // reads (8 rows x 32 B per half-wave) spread over distinct banks.
+// A half-wave tr16 read touches rows {b..b+3} u {b+8..b+11}: with 256-B rows the XOR key
+// (row&3, bit3) separates them; with 128-B rows row parity already splits the 256-B bank cycle, so
+// the 2-bit key is (bit1, bit3).
 template <int NWIN>
 __device__ __forceinline__ int tn_swz(int row, int win) {
-  return win ^ (((row & 3) | (((row >> 3) & 1) << 2)) & (NWIN - 1));
+  if constexpr (NWIN >= 8) return win ^ ((row & 3) | (((row >> 3) & 1) << 2));
+  else return win ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) & (NWIN - 1));
 }
 
 // LDS-DMA ring like the NT kernel: one wave-instruction fills 1 KiB = 1024/ROWB pixel rows; lane
@@ -403,9 +407,14 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int tile_m = blockIdx.x / a.ntn, tile_n = blockIdx.x % a.ntn;
+  // 1-D grid over (split, tile), tile fastest.  (Grouping a split's tiles on one XCD cuts the
+  // layer-1 HBM fetch 4.6x but ran 1.3x slower: the kernel is issue-bound, not HBM-bound, and
+  // the grouped blocks contend for the same L2 lines.)
+  const int ntiles = a.ntm * a.ntn;
+  const int split = blockIdx.x / ntiles, tile = blockIdx.x - split * ntiles;
+  const int tile_m = tile / a.ntn, tile_n = tile % a.ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;  // m: kout, n: (tap, c)
-  const int p_begin = blockIdx.y * a.kchunk;
+  const int p_begin = split * a.kchunk;
   const int p_end = min(p_begin + a.kchunk, g.M);
 
   // Buffer-descriptor LDS-DMA loads (out-of-range voffset -> zeros).  Per (lane, instruction) the
@@ -574,7 +583,7 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   }
 
   // epilogue: slab[split][kout = m][n..n+3]
-  float* __restrict__ slab = a.slab + (size_t)blockIdx.y * a.Kout * a.Ng;
+  float* __restrict__ slab = a.slab + (size_t)split * a.Kout * a.Ng;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WN + 16 * j + 4 * fq;
@@ -913,7 +922,7 @@ int launch_tn(TNArgs a, const TNPlan& p, hipStream_t st) {
   a.ntm = p.ntm;
   a.ntn = p.ntn;
   a.kchunk = p.kchunk;
-  const dim3 grid(p.ntm * p.ntn, p.splits), blk(256);
+  const dim3 grid(p.ntm * p.ntn * p.splits), blk(256);
   if (p.bm == 128 && p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, a);
   else if (p.bm == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, a);
   else if (p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, a);
