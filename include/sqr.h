@@ -123,6 +123,11 @@ int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_de
  * stats must hold sqr_conv2d_stats_floats(d) floats.  Feed them to sqr_bn_fwd_stats /
  * sqr_stem_fwd_stats so the BatchNorm that follows the conv never re-reads the activation. */
 size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
+/* Routing of bf16 3x3/stride-1/pad-1 forward and backward-data convs to the direct halo-window
+ * kernel: 1 (default) when the shape tiles and the grid fills the chip, 2 whenever the shape
+ * tiles, 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.
+ * Process-wide; meant for A/B tests. */
+int sqr_conv_set_direct(int mode);
 int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
                          int* stats_rows, void* workspace, size_t workspace_bytes, void* stream);
 /* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1

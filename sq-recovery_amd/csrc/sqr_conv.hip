@@ -27,17 +27,10 @@
 // Convs whose input has < 8 channels (conv1: C=1) run as an explicit im2col (K padded to 64) +
 // 1x1 GEMM through the same kernels.
 #include <stdint.h>
-#include "sqr_common.h"
+#include "sqr_conv_dev.h"
 
 namespace sqr {
 namespace conv {
-
-typedef __bf16 bf16;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // implicit im2col view of an NHWC tensor
 struct Gather {
@@ -72,59 +65,9 @@ struct TNArgs {
   int rect_wt;       // > 0: every BK-pixel tile is a rect_wt-wide rectangle of one image (no divides)
 };
 
-template <typename T> struct Cfg;
-template <> struct Cfg<bf16> {
-  static constexpr int ES = 2, VEC = 8, KSUB = 32;
-};
-template <> struct Cfg<float> {
-  static constexpr int ES = 4, VEC = 4, KSUB = 4;
-};
-
-__device__ __forceinline__ int nt_swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
-
-// bijective XCD-aware remap: blocks b and b+8 share an XCD, give each XCD a contiguous id range
-__device__ __forceinline__ int xcd_remap(int b, int nb) {
-  const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-}
-
-__device__ __forceinline__ void store4(bf16* p, const f32x4& v) {
-  typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  bf16x4 o;
-  o[0] = (bf16)v[0];
-  o[1] = (bf16)v[1];
-  o[2] = (bf16)v[2];
-  o[3] = (bf16)v[3];
-  *(bf16x4*)p = o;
-}
-__device__ __forceinline__ void store4(float* p, const f32x4& v) { *(f32x4*)p = v; }
-
-__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-__device__ __forceinline__ f32x4 mfma(float a, float b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
 // ============================================================================ NT (fwd / dgrad)
 // 16-B zero source for LDS-DMA lanes whose im2col element lies in the padding
 __device__ __attribute__((aligned(64))) unsigned int g_zero16[16];
-
-// transposing LDS read (gfx950 ds_read_b64_tr_b16) as inline asm: the builtin form makes hipcc
-// wait vmcnt(0) for every in-flight LDS-DMA before it (it cannot rule out aliasing), which would
-// serialise the DMA ring.  The caller waits lgkmcnt itself (tr_wait) before using the results.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void*)p);
-}
-__device__ __forceinline__ s16x4 ds_read_tr16(uint32_t addr) {
-  s16x4 r;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
-__device__ __forceinline__ void tr_wait() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_row_block) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_row_block, 16, 0, 0);
@@ -1002,6 +945,10 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
   a.oph = a.opw = 0;
   a.oH = sh.Ho;
   a.oW = sh.Wo;
+  if (!sh.im2col && d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1) {
+    rc = conv3_launch(x, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, st);
+    if (rc != 1) return rc;  // launched (0) or failed; 1 = shape not covered by the direct kernel
+  }
   a.stats = stats;
   if (stats_rows) *stats_rows = (sh.M + ((nt_cfg(sh.M, d->K) <= 1) ? 128 : 64) - 1) / ((nt_cfg(sh.M, d->K) <= 1) ? 128 : 64);
   if (sh.im2col) {
@@ -1066,6 +1013,10 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
   SQR_CHECK_ARG(!sh.im2col, "conv2d_bwd_data: C=%d < 8 not supported", d->C);
   SQR_CHECK_ARG(dy && w_crsk && dx, "conv2d_bwd_data: null pointer");
   hipStream_t st = as_stream(stream);
+  if (d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1) {
+    rc = conv3_launch(dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, st);
+    if (rc != 1) return rc;
+  }
   // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+p-r)/st,(w+p-s)/st,k] W[k,c,r,s] over the divisible taps.
   // Output pixels split by parity (h%st, w%st); in class (ph,pw) only taps r = r0 + st*t contribute
   // and dY row = i + off_h - t: a stride-1 implicit GEMM over the class grid (Hc x Wc).

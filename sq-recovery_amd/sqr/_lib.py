@@ -46,6 +46,7 @@ SIGNATURES = {
     "sqr_conv2d_pack_weights": (c_int, [ctypes.POINTER(SqrPackJob), c_int, c_void_p]),
     "sqr_conv2d_fwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t,
                                c_void_p]),
+    "sqr_conv_set_direct": (c_int, [c_int]),
     "sqr_conv2d_stats_floats": (c_size_t, [ctypes.POINTER(SqrConvDesc)]),
     "sqr_conv2d_fwd_stats": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                      ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),

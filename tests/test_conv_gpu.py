@@ -114,3 +114,52 @@ def test_conv_deterministic():
         outs.append((y.clone(), x.grad.clone(), w.grad.clone()))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+# direct 3x3/s1/p1 kernel (sqr_conv3.hip): one shape per tile configuration (and multi-tile rows,
+# Cin != Nout); forced on (mode 2) so the small test batches take it, and compared with the
+# implicit-GEMM path (mode 0) and the float64 reference
+DIRECT = [
+    (2, 64, 64, 64),     # cfg 0 (TW 64 x TH 4, single window)
+    (1, 64, 128, 64),    # cfg 0, two tiles per image row
+    (2, 128, 32, 128),   # cfg 1 (TW 32 x TH 8, double-buffered window, 2 chunks)
+    (1, 128, 64, 128),   # cfg 1, two tiles per row
+    (2, 256, 16, 256),   # cfg 2 (TW 16 x TH 8)
+    (2, 512, 8, 512),    # cfg 3 (8 x 8, 8 chunks)
+    (2, 128, 16, 256),   # Cin != Nout
+    (2, 64, 32, 128),    # fwd direct (cfg 1, one chunk); dgrad falls back
+]
+
+
+@pytest.mark.parametrize("shape", DIRECT, ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv3_direct(shape):
+    from sqr import conv as sc
+    from sqr._lib import lib
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(N + C + H + K)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    gy = torch.randn(N, K, H, H, generator=g).bfloat16().float()
+    yr, dxr, dwr = _ref(x, w.bfloat16().float(), 1, 1, gy)
+    res = {}
+    old = lib().sqr_conv_set_direct(2)
+    try:
+        for mode in (2, 0):
+            lib().sqr_conv_set_direct(mode)
+            xg = x.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            wg = w.to(DEV).requires_grad_(True)
+            y, st = sc.conv2d(xg, wg, None, 1, 1, stats=True)
+            y.backward(gy.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last))
+            torch.cuda.synchronize()
+            res[mode] = (y.float(), xg.grad.float(), st.double().sum(0))
+    finally:
+        lib().sqr_conv_set_direct(old)
+    for mode in (2, 0):
+        y, dx, st = res[mode]
+        assert _rel(y, yr) <= 8e-3
+        assert _rel(dx, dxr) <= 8e-3
+        yd = y.double()
+        assert _rel(st[0], yd.sum((0, 2, 3))) <= 1e-5
+        assert _rel(st[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
+    assert _rel(res[2][0], res[0][0]) <= 8e-3
+    assert _rel(res[2][1], res[0][1]) <= 8e-3
