@@ -131,6 +131,8 @@ class ResNetSQ(nn.Module):
         self.output_rotation = RotationHead(self.fcn)
 
     def forward(self, x):
-        x = self.encoder(_cl(x))
-        return (self.output_size.forward(x), self.output_shape.forward(x), self.output_position.forward(x),
-                self.output_rotation.forward(x))
+        x = self.encoder(_cl(x))  # fp32 features (the encoder's MLP tail runs in fp32)
+        with torch.autocast("cuda", enabled=False):
+            x = x.float()
+            return (self.output_size.forward(x), self.output_shape.forward(x), self.output_position.forward(x),
+                    self.output_rotation.forward(x))

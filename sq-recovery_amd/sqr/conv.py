@@ -197,6 +197,9 @@ def compute_dtype(x):
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False):
+        # the statistics output is non-differentiable: don't let autograd materialise a zero
+        # gradient tensor for it in backward
+        ctx.set_materialize_grads(False)
         N, C, H, W = x.shape
         K, _, R, S = weight.shape
         xin = x.to(dt).contiguous(memory_format=_CL)
@@ -227,6 +230,8 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, *_):
+        if gy is None:  # grads are not materialised (see forward)
+            return None, None, None, None, None, None, None, None
         xin, crsk, col = ctx.saved_tensors
         d = ctx.d
         dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32

@@ -82,8 +82,11 @@ class ResNet18(nn.Module):
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             clear_packed(convs)  # packed weights live on in autograd's saved tensors only
-        x = torch.flatten(self.avgpool(x), 1)
-        return self.fc(x)
+        # the 512-feature MLP tail is tiny: run it in fp32 even under bf16 autocast (one fp32
+        # average-pool read of the bf16 activation instead of a cast kernel per Linear)
+        x = x.mean((2, 3), dtype=torch.float32) if x.is_cuda else torch.flatten(self.avgpool(x), 1)
+        with torch.autocast("cuda", enabled=False):
+            return self.fc(x)
 
 
 def resnet18(pretrained=False):
