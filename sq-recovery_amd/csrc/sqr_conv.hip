@@ -318,14 +318,6 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
 // ============================================================================ TN (wgrad)
 // LDS tiles [BK pixels][cols]; 32-byte windows XOR-swizzled by row so that the transposing
 // reads (8 rows x 32 B per half-wave) spread over distinct banks.
-// A half-wave tr16 read touches rows {b..b+3} u {b+8..b+11}: with 256-B rows the XOR key
-// (row&3, bit3) separates them; with 128-B rows row parity already splits the 256-B bank cycle, so
-// the 2-bit key is (bit1, bit3).
-template <int NWIN>
-__device__ __forceinline__ int tn_swz(int row, int win) {
-  if constexpr (NWIN >= 8) return win ^ ((row & 3) | (((row >> 3) & 1) << 2));
-  else return win ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) & (NWIN - 1));
-}
 
 // LDS-DMA ring like the NT kernel: one wave-instruction fills 1 KiB = 1024/ROWB pixel rows; lane
 // l lands in physical 16-B chunk l % (ROWB/16) of its row and loads the logical chunk given by the
@@ -889,6 +881,11 @@ extern "C" int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo) {
   return 0;
 }
 
+// bf16 3x3 / stride 1 / pad 1 (the direct kernels' domain; they decline other shapes themselves)
+static bool direct3(const sqr_conv_desc* d, const Shape& sh) {
+  return !sh.im2col && d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1;
+}
+
 extern "C" size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which) {
   Shape sh;
   if (check_desc(d, &sh)) return 0;
@@ -897,7 +894,12 @@ extern "C" size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which) 
   if (which == 1) return 0;
   const int Ng = sh.im2col ? sh.Kp : d->R * d->S * d->C;
   const TNPlan p = plan_tn(d->K, Ng, sh.M, sh.ES);
-  return col + align_up((size_t)p.splits * d->K * Ng * sizeof(float));
+  size_t slab = (size_t)p.splits * d->K * Ng * sizeof(float);
+  if (direct3(d, sh)) {
+    const size_t s3 = conv3w_slab_bytes(d->N, d->H, d->W, d->C, d->K);
+    slab = s3 > slab ? s3 : slab;
+  }
+  return col + align_up(slab);
 }
 
 extern "C" int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* d, void* w_krsc, void* w_crsk,
@@ -1076,6 +1078,19 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   } else {
     a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, -d->pad, 1, d->R, d->S, d->N, sh.ES);
     Ng = d->R * d->S * d->C;
+  }
+  if (direct3(d, sh)) {
+    int splits = 0;
+    const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
+    rc = conv3w_launch(x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
+    if (rc == 0) {
+      const int total = d->K * (Ng / 4);
+      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, st, (const float*)ws, splits,
+                         d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs);
+      SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
+      return 0;
+    }
+    if (rc != 1) return rc;
   }
   a.dy = dy;
   a.Kout = d->K;

@@ -249,6 +249,193 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
                                                  a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
 }
 
+
+// ============================================================================ weight gradient
+// dW[k][tap][c] = sum_p dY[p][k] * X[p + shift(tap)][c] over the pixels of the split.  A
+// workgroup owns a 64 (k) x 64 (c) x 9 (taps) output block and walks its split's pixel chunks
+// (TH x TW rectangles of one image): per chunk it stages the dY rows and the (TH+2) x (TW+2) X halo
+// window (both pixel-major, 128-B rows, 32-B-window XOR swizzle) and runs 9 shifted GEMMs whose
+// MFMA fragments come from ds_read_b64_tr_b16 transposing reads.  Wave w owns channels
+// c0+16w..+15 for all 4 k-tiles and 9 taps: per 32-pixel k-step 4 dY + 9 X fragments feed
+// 36 MFMAs, and per chunk one window serves all 9 taps (the implicit-GEMM TN kernel re-gathers X
+// per tap).  Output: fp32 split slabs in the TN layout, reduced by wgrad_reduce_kernel.
+struct D3WArgs {
+  const void* x;   // [N][H][W][C]
+  const void* dy;  // [N][H][W][K]
+  float* slab;     // [splits][K][9*C]
+  int N, H, W, C, K;
+  int tiles_x, chunks_per_img, nchunks, cps;  // cps = chunks per split
+  int ntc, ntiles;                              // C/64, (K/64)*(C/64)
+  uint32_t xbytes, dybytes;
+};
+
+template <int TW, int TH, int STAGES>
+__global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
+  constexpr int NW = 4, ROWB = 128;
+  constexpr int BKP = TW * TH, SUBS = BKP / 32;      // pixels per chunk, 32-pixel k-steps
+  constexpr int WWID = TW + 2, WR = (TH + 2) * WWID;
+  constexpr int WROWS = (WR + 31) / 32 * 32;
+  constexpr int DP = BKP / 32, XP = WROWS / 32;      // dY / window pieces per wave per chunk
+  constexpr int PER = DP + XP;
+  constexpr int TILE_D = BKP * ROWB, STAGE = TILE_D + WROWS * ROWB;
+  static_assert(BKP % 64 == 0, "chunk = multiple of 64 pixels");
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / a.ntiles, tile = bid - split * a.ntiles;
+  const int k0 = (tile / a.ntc) * 64, c0 = (tile % a.ntc) * 64;
+  const int ch0 = split * a.cps;
+  const int nloc = min(a.nchunks - ch0, a.cps);
+
+  // ---- per-lane DMA constants
+  constexpr uint32_t kOOB = 0x80000000u;
+  const int prow = lane >> 3, pslot = lane & 7;
+  uint32_t dvoff[DP];  // dY: chunk-relative byte offset (the chunk origin goes in soffset)
+#pragma unroll
+  for (int i = 0; i < DP; ++i) {
+    const int r = (i * NW + wave) * 8 + prow;  // local pixel
+    const int lch = 2 * tn_swz<4>(r, pslot >> 1) + (pslot & 1);
+    dvoff[i] = (uint32_t)((((r / TW) * a.W + (r % TW)) * a.K + k0 + lch * 8) * 2);
+  }
+  int xwy[XP], xwx[XP], xcol[XP];
+#pragma unroll
+  for (int i = 0; i < XP; ++i) {
+    const int r = (i * NW + wave) * 8 + prow;  // window row
+    const int lch = 2 * tn_swz<4>(r, pslot >> 1) + (pslot & 1);
+    xwy[i] = r < WR ? r / WWID : -(1 << 20);  // padding rows of the LDS window fail the bounds test
+    xwx[i] = r % WWID;
+    xcol[i] = (c0 + lch * 8) * 2;
+  }
+  const __amdgpu_buffer_rsrc_t xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, a.dybytes, 0x00020000);
+
+#define SQR_W_ISSUE(q_, stage_)                                                                              \
+  do {                                                                                                     \
+    const int ch = ch0 + (q_);                                                                             \
+    const int img = ch / a.chunks_per_img, rem = ch - img * a.chunks_per_img;                              \
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;                                             \
+    const int h0 = ty * TH, w0 = tx * TW;                                                                  \
+    char* dst_ = smem + (stage_) * STAGE;                                                                  \
+    const int dso = __builtin_amdgcn_readfirstlane(((img * a.H + h0) * a.W + w0) * a.K * 2);               \
+    dma_pieces<DP, NW>(dsrd, dst_, dvoff, dso, wave);                                                      \
+    uint32_t xvo[XP];                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < XP; ++i) {                                                       \
+      const int h = h0 - 1 + xwy[i], w = w0 - 1 + xwx[i];                                                  \
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;                          \
+      xvo[i] = ok ? (uint32_t)(((img * a.H + h) * a.W + w) * a.C * 2 + xcol[i]) : kOOB;                    \
+    }                                                                                                      \
+    dma_pieces<XP, NW>(xsrd, dst_ + TILE_D, xvo, 0, wave);                                                 \
+  } while (0)
+
+  // ---- fragment addressing: lane (fq, fr) reads k-rows kk = 32*sub + 8*fq + (fr>>2) (+4) and
+  // 4 columns at byte cb (TN kernel convention)
+  const int fr = lane & 15, fq = lane >> 4;
+  int draddr[SUBS][2][4];  // dY fragment byte offsets inside a stage (k-tile kt)
+  int xrow[SUBS][2];       // window row of pixel kk at tap shift (0, 0)
+#pragma unroll
+  for (int sub = 0; sub < SUBS; ++sub)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kk = 32 * sub + 8 * fq + (fr >> 2) + 4 * h;
+      xrow[sub][h] = (kk / TW) * WWID + (kk % TW);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const int cb = (16 * kt + 4 * (fr & 3)) * 2;
+        draddr[sub][h][kt] = kk * ROWB + tn_swz<4>(kk, cb >> 5) * 32 + (cb & 31);
+      }
+    }
+  const int xcb = (16 * wave + 4 * (fr & 3)) * 2;
+
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) acc[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int q = 0; q < STAGES - 1; ++q)
+    if (q < nloc) SQR_W_ISSUE(q, q);
+  if (nloc >= STAGES - 1) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (STAGES - 2)) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  for (int q = 0; q < nloc; ++q) {
+    const bool more = q + STAGES - 1 < nloc;
+    if (more) SQR_W_ISSUE(q + STAGES - 1, (q + STAGES - 1) % STAGES);
+    const char* dst = smem + (q % STAGES) * STAGE;
+    const char* xw = dst + TILE_D;
+#pragma unroll
+    for (int sub = 0; sub < SUBS; ++sub) {
+      // software pipeline (one wave per SIMD: nothing else hides LDS latency): the dY fragments
+      // and the X fragments of taps 0-1 are requested up front, then tap t+2's reads are issued
+      // behind tap t's 4 MFMAs and a counted lgkmcnt leaves them in flight
+      s16x4 dlo[4], dhi[4], xlo[9], xhi[9];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        dlo[kt] = ds_read_tr16(lds_addr(dst + draddr[sub][0][kt]));
+        dhi[kt] = ds_read_tr16(lds_addr(dst + draddr[sub][1][kt]));
+      }
+#define SQR_X_READ(t)                                                                              \
+  do {                                                                                             \
+    int r0 = xrow[sub][0] + ((t) / 3) * WWID + ((t) % 3), r1 = xrow[sub][1] + ((t) / 3) * WWID + ((t) % 3); \
+    asm volatile("" : "+v"(r0), "+v"(r1));                                                         \
+    xlo[t] = ds_read_tr16(lds_addr(xw + r0 * ROWB + tn_swz<4>(r0, xcb >> 5) * 32 + (xcb & 31)));   \
+    xhi[t] = ds_read_tr16(lds_addr(xw + r1 * ROWB + tn_swz<4>(r1, xcb >> 5) * 32 + (xcb & 31)));   \
+  } while (0)
+      SQR_X_READ(0);
+      SQR_X_READ(1);
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const s16x8 v = {dlo[kt][0], dlo[kt][1], dlo[kt][2], dlo[kt][3], dhi[kt][0], dhi[kt][1], dhi[kt][2], dhi[kt][3]};
+        bfr[kt] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const s16x8 v = {xlo[t][0], xlo[t][1], xlo[t][2], xlo[t][3], xhi[t][0], xhi[t][1], xhi[t][2], xhi[t][3]};
+        const bf16x8 afr = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) acc[t][kt] = mfma(afr, bfr[kt], acc[t][kt]);
+        if (t + 2 < 9) {
+          SQR_X_READ(t + 2 < 9 ? t + 2 : 8);
+          asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#undef SQR_X_READ
+    }
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (STAGES - 2)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+
+#undef SQR_W_ISSUE
+
+  // ---- epilogue: lane holds dW[k = k0+16kt+fr][tap t][c = c0+16w+4fq .. +3]
+  const size_t ng = (size_t)9 * a.C;
+  float* __restrict__ slab = a.slab + (size_t)split * a.K * ng;
+  const int c = c0 + 16 * wave + 4 * fq;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt) {
+    float* row = slab + (size_t)(k0 + 16 * kt + fr) * ng + c;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) *(f32x4*)(row + t * a.C) = acc[t][kt];
+  }
+}
+
 namespace {
 struct D3Cfg {
   int id, BM, BN, threads, TW, TH, nwb;
@@ -325,6 +512,70 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
     default: hipLaunchKernelGGL((conv3_kernel<64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
   }
   SQR_HIP_LAUNCH_CHECK("conv3_kernel");
+  return 0;
+}
+
+// ---------------------------------------------------------------- weight-gradient launcher
+namespace {
+struct D3WPlan {
+  int TW, TH, splits, cps, nchunks, chunks_per_img, tiles_x, ntiles;
+};
+bool plan_w(int N, int H, int W, int C, int K, D3WPlan* p) {
+  if (g_direct == 0 || C % 64 || K % 64 || W < 8 || pow2_log(W) < 0) return false;
+  const int TW = W >= 64 ? 64 : W, TH = 64 / TW;  // 64-pixel chunks
+  if (H % TH) return false;
+  if ((size_t)N * H * W * (C > K ? C : K) * 2 >= (1u << 31)) return false;
+  p->TW = TW;
+  p->TH = TH;
+  p->tiles_x = W / TW;
+  p->chunks_per_img = (H / TH) * p->tiles_x;
+  p->nchunks = N * p->chunks_per_img;
+  p->ntiles = (K / 64) * (C / 64);
+  int splits = (256 + p->ntiles - 1) / p->ntiles;  // one workgroup per CU
+  splits = splits > p->nchunks ? p->nchunks : splits;
+  p->cps = (p->nchunks + splits - 1) / splits;
+  p->splits = (p->nchunks + p->cps - 1) / p->cps;
+  return true;
+}
+}  // namespace
+
+size_t conv3w_slab_bytes(int N, int H, int W, int C, int K) {
+  D3WPlan p;
+  if (!plan_w(N, H, W, C, K, &p)) return 0;
+  return (size_t)p.splits * K * 9 * C * sizeof(float);
+}
+
+int conv3w_launch(const void* x, const void* dy, float* slab, size_t slab_bytes, int N, int H, int W, int C, int K,
+                  int* splits, hipStream_t st) {
+  D3WPlan p;
+  if (!plan_w(N, H, W, C, K, &p)) return 1;
+  if ((size_t)p.splits * K * 9 * C * sizeof(float) > slab_bytes) return 1;
+  D3WArgs a;
+  a.x = x;
+  a.dy = dy;
+  a.slab = slab;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.K = K;
+  a.tiles_x = p.tiles_x;
+  a.chunks_per_img = p.chunks_per_img;
+  a.nchunks = p.nchunks;
+  a.cps = p.cps;
+  a.ntc = C / 64;
+  a.ntiles = p.ntiles;
+  a.xbytes = (uint32_t)((size_t)N * H * W * C * 2);
+  a.dybytes = (uint32_t)((size_t)N * H * W * K * 2);
+  *splits = p.splits;
+  const dim3 grid(p.splits * p.ntiles), blk(256);
+  switch (p.TW) {
+    case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<64, 1, 3>), grid, blk, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<32, 2, 3>), grid, blk, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<16, 4, 3>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3_wgrad_kernel<8, 8, 3>), grid, blk, 0, st, a); break;
+  }
+  SQR_HIP_LAUNCH_CHECK("conv3_wgrad_kernel");
   return 0;
 }
 

@@ -63,10 +63,24 @@ __device__ __forceinline__ void tr_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// A half-wave tr16 read touches rows {b..b+3} u {b+8..b+11}: with 256-B rows the XOR key
+// (row&3, bit3) separates them; with 128-B rows row parity already splits the 256-B bank cycle, so
+// the 2-bit key is (bit1, bit3).
+template <int NWIN>
+__device__ __forceinline__ int tn_swz(int row, int win) {
+  if constexpr (NWIN >= 8) return win ^ ((row & 3) | (((row >> 3) & 1) << 2));
+  else return win ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) & (NWIN - 1));
+}
+
 // direct 3x3/s1/p1 bf16 kernel (sqr_conv3.hip): 1 = shape not handled (use the implicit-GEMM
 // path), 0 = launched, otherwise an error code
 int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st);
+// direct 3x3/s1/p1 bf16 weight gradient: fp32 slabs [splits][K][9*C] ((tap, c) columns, the
+// implicit-GEMM TN layout) for wgrad_reduce_kernel.  conv3w_slab_bytes = 0 if not handled.
+size_t conv3w_slab_bytes(int N, int H, int W, int C, int K);
+int conv3w_launch(const void* x, const void* dy, float* slab, size_t slab_bytes, int N, int H, int W, int C, int K,
+                  int* splits, hipStream_t st);
 
 }  // namespace conv
 }  // namespace sqr

@@ -151,15 +151,17 @@ def test_conv3_direct(shape):
             y, st = sc.conv2d(xg, wg, None, 1, 1, stats=True)
             y.backward(gy.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last))
             torch.cuda.synchronize()
-            res[mode] = (y.float(), xg.grad.float(), st.double().sum(0))
+            res[mode] = (y.float(), xg.grad.float(), st.double().sum(0), wg.grad.clone())
     finally:
         lib().sqr_conv_set_direct(old)
     for mode in (2, 0):
-        y, dx, st = res[mode]
+        y, dx, st, dw = res[mode]
         assert _rel(y, yr) <= 8e-3
         assert _rel(dx, dxr) <= 8e-3
+        assert _rel(dw, dwr) <= 2e-4
         yd = y.double()
         assert _rel(st[0], yd.sum((0, 2, 3))) <= 1e-5
         assert _rel(st[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
     assert _rel(res[2][0], res[0][0]) <= 8e-3
     assert _rel(res[2][1], res[0][1]) <= 8e-3
+    assert _rel(res[2][3], res[0][3]) <= 2e-4
