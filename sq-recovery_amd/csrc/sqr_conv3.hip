@@ -259,6 +259,20 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 // c0+16w..+15 for all 4 k-tiles and 9 taps: per 32-pixel k-step 4 dY + 9 X fragments feed
 // 36 MFMAs, and per chunk one window serves all 9 taps (the implicit-GEMM TN kernel re-gathers X
 // per tap).  Output: fp32 split slabs in the TN layout, reduced by wgrad_reduce_kernel.
+// 32-B-window XOR key of an LDS pixel row by its (y, x) position in the tile/window:
+// the half-wave tr16 reads touch pixels (y, x..x+3) and (y, x+8..x+11) (TW >= 16) or
+// (y, x..x+3) and (y+1, x..x+3) (TW = 8); with 128-B rows the row parity (= x parity, widths are
+// even) splits the 256-B bank cycle and this key separates the rest.  Because it depends on x and
+// on the parity of y only, a tap shift by r rows keeps it (r even) or flips its bit 1 (r odd).
+__device__ __forceinline__ int psw(int y, int x) { return ((x >> 1) & 1) | ((((x >> 3) ^ y) & 1) << 1); }
+
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_read_tr16_off(uint32_t addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+
 struct D3WArgs {
   const void* x;   // [N][H][W][C]
   const void* dy;  // [N][H][W][K]
@@ -296,14 +310,14 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
 #pragma unroll
   for (int i = 0; i < DP; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // local pixel
-    const int lch = 2 * tn_swz<4>(r, pslot >> 1) + (pslot & 1);
+    const int lch = 2 * ((pslot >> 1) ^ psw(r / TW, r % TW)) + (pslot & 1);
     dvoff[i] = (uint32_t)((((r / TW) * a.W + (r % TW)) * a.K + k0 + lch * 8) * 2);
   }
   int xwy[XP], xwx[XP], xcol[XP];
 #pragma unroll
   for (int i = 0; i < XP; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // window row
-    const int lch = 2 * tn_swz<4>(r, pslot >> 1) + (pslot & 1);
+    const int lch = 2 * ((pslot >> 1) ^ psw(r / WWID, r % WWID)) + (pslot & 1);
     xwy[i] = r < WR ? r / WWID : -(1 << 20);  // padding rows of the LDS window fail the bounds test
     xwx[i] = r % WWID;
     xcol[i] = (c0 + lch * 8) * 2;
@@ -329,24 +343,23 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     dma_pieces<XP, NW>(xsrd, dst_ + TILE_D, xvo, 0, wave);                                                 \
   } while (0)
 
-  // ---- fragment addressing: lane (fq, fr) reads k-rows kk = 32*sub + 8*fq + (fr>>2) (+4) and
-  // 4 columns at byte cb (TN kernel convention)
+  // ---- fragment addressing: lane (fq, fr) reads pixels kk = 32*sub + 8*fq + (fr>>2) (+4) at
+  // byte 8*(fr&3) of the 32-B window holding its 16 columns (TN kernel convention)
   const int fr = lane & 15, fq = lane >> 4;
-  int draddr[SUBS][2][4];  // dY fragment byte offsets inside a stage (k-tile kt)
-  int xrow[SUBS][2];       // window row of pixel kk at tap shift (0, 0)
+  int draddr[SUBS][2][4];  // dY fragment offsets in a stage, k-tile kt
+  int xaddr[SUBS][2][3];   // window fragment offsets at tap (0, s); tap (r, s) = +r rows, ^64 if r odd
 #pragma unroll
   for (int sub = 0; sub < SUBS; ++sub)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int kk = 32 * sub + 8 * fq + (fr >> 2) + 4 * h;
-      xrow[sub][h] = (kk / TW) * WWID + (kk % TW);
+      const int py = kk / TW, px = kk % TW;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        const int cb = (16 * kt + 4 * (fr & 3)) * 2;
-        draddr[sub][h][kt] = kk * ROWB + tn_swz<4>(kk, cb >> 5) * 32 + (cb & 31);
-      }
+      for (int kt = 0; kt < 4; ++kt) draddr[sub][h][kt] = kk * ROWB + ((kt ^ psw(py, px)) << 5) + 8 * (fr & 3);
+#pragma unroll
+      for (int c3 = 0; c3 < 3; ++c3)
+        xaddr[sub][h][c3] = (py * WWID + px + c3) * ROWB + ((wave ^ psw(py, px + c3)) << 5) + 8 * (fr & 3);
     }
-  const int xcb = (16 * wave + 4 * (fr & 3)) * 2;
 
   f32x4 acc[9][4];
 #pragma unroll
@@ -368,8 +381,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   for (int q = 0; q < nloc; ++q) {
     const bool more = q + STAGES - 1 < nloc;
     if (more) SQR_W_ISSUE(q + STAGES - 1, (q + STAGES - 1) % STAGES);
-    const char* dst = smem + (q % STAGES) * STAGE;
-    const char* xw = dst + TILE_D;
+    const uint32_t dbase = lds_addr(smem + (q % STAGES) * STAGE), xbase = dbase + TILE_D;
 #pragma unroll
     for (int sub = 0; sub < SUBS; ++sub) {
       // software pipeline (one wave per SIMD: nothing else hides LDS latency): the dY fragments
@@ -378,15 +390,22 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
       s16x4 dlo[4], dhi[4], xlo[9], xhi[9];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        dlo[kt] = ds_read_tr16(lds_addr(dst + draddr[sub][0][kt]));
-        dhi[kt] = ds_read_tr16(lds_addr(dst + draddr[sub][1][kt]));
+        dlo[kt] = ds_read_tr16(dbase + draddr[sub][0][kt]);
+        dhi[kt] = ds_read_tr16(dbase + draddr[sub][1][kt]);
       }
-#define SQR_X_READ(t)                                                                              \
-  do {                                                                                             \
-    int r0 = xrow[sub][0] + ((t) / 3) * WWID + ((t) % 3), r1 = xrow[sub][1] + ((t) / 3) * WWID + ((t) % 3); \
-    asm volatile("" : "+v"(r0), "+v"(r1));                                                         \
-    xlo[t] = ds_read_tr16(lds_addr(xw + r0 * ROWB + tn_swz<4>(r0, xcb >> 5) * 32 + (xcb & 31)));   \
-    xhi[t] = ds_read_tr16(lds_addr(xw + r1 * ROWB + tn_swz<4>(r1, xcb >> 5) * 32 + (xcb & 31)));   \
+      uint32_t xb[2][3], xb1[2][3];  // tap rows r even / odd
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int c3 = 0; c3 < 3; ++c3) {
+          xb[h][c3] = xbase + xaddr[sub][h][c3];
+          xb1[h][c3] = xb[h][c3] ^ 64u;
+        }
+#define SQR_X_READ(T)                                                                                 \
+  do {                                                                                                \
+    constexpr int R_ = (T) / 3, S_ = (T) % 3, OFF_ = R_ * WWID * ROWB;                                \
+    xlo[T] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[0][S_] : xb[0][S_]);                                \
+    xhi[T] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[1][S_] : xb[1][S_]);                                \
   } while (0)
       SQR_X_READ(0);
       SQR_X_READ(1);
@@ -398,20 +417,32 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
         const s16x8 v = {dlo[kt][0], dlo[kt][1], dlo[kt][2], dlo[kt][3], dhi[kt][0], dhi[kt][1], dhi[kt][2], dhi[kt][3]};
         bfr[kt] = __builtin_bit_cast(bf16x8, v);
       }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const s16x8 v = {xlo[t][0], xlo[t][1], xlo[t][2], xlo[t][3], xhi[t][0], xhi[t][1], xhi[t][2], xhi[t][3]};
-        const bf16x8 afr = __builtin_bit_cast(bf16x8, v);
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) acc[t][kt] = mfma(afr, bfr[kt], acc[t][kt]);
-        if (t + 2 < 9) {
-          SQR_X_READ(t + 2 < 9 ? t + 2 : 8);
-          asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+#define SQR_TAP(T)                                                                                     \
+  do {                                                                                                 \
+    const s16x8 v_ = {xlo[T][0], xlo[T][1], xlo[T][2], xlo[T][3], xhi[T][0], xhi[T][1], xhi[T][2], xhi[T][3]}; \
+    const bf16x8 afr_ = __builtin_bit_cast(bf16x8, v_);                                                \
+    _Pragma("unroll") for (int kt = 0; kt < 4; ++kt) acc[T][kt] = mfma(afr_, bfr[kt], acc[T][kt]);     \
+  } while (0)
+#define SQR_TAP_NEXT(T)                                  \
+  do {                                                   \
+    SQR_TAP(T);                                          \
+    SQR_X_READ(T + 2);                                   \
+    asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");   \
+    __builtin_amdgcn_sched_barrier(0);                   \
+  } while (0)
+      SQR_TAP_NEXT(0);
+      SQR_TAP_NEXT(1);
+      SQR_TAP_NEXT(2);
+      SQR_TAP_NEXT(3);
+      SQR_TAP_NEXT(4);
+      SQR_TAP_NEXT(5);
+      SQR_TAP_NEXT(6);
+      SQR_TAP(7);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      SQR_TAP(8);
+#undef SQR_TAP_NEXT
+#undef SQR_TAP
 #undef SQR_X_READ
     }
     if (more) {
