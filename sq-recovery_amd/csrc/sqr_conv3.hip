@@ -20,6 +20,10 @@
 #include <stdint.h>
 #include "sqr_conv_dev.h"
 
+#ifndef SQR_EXP
+#define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop)
+#endif
+
 namespace sqr {
 namespace conv {
 
@@ -380,7 +384,11 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   for (int q = 0; q < nloc; ++q) {
     const bool more = q + STAGES - 1 < nloc;
+#if SQR_EXP & 2
+    (void)more;
+#else
     if (more) SQR_W_ISSUE(q + STAGES - 1, (q + STAGES - 1) % STAGES);
+#endif
     const uint32_t dbase = lds_addr(smem + (q % STAGES) * STAGE), xbase = dbase + TILE_D;
 #pragma unroll
     for (int sub = 0; sub < SUBS; ++sub) {
@@ -459,12 +467,21 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   const size_t ng = (size_t)9 * a.C;
   float* __restrict__ slab = a.slab + (size_t)split * a.K * ng;
   const int c = c0 + 16 * wave + 4 * fq;
+#if SQR_EXP & 1
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) sum += acc[t][kt][0] + acc[t][kt][1] + acc[t][kt][2] + acc[t][kt][3];
+  if (sum == 1234.5f) slab[tid] = sum;
+#else
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt) {
     float* row = slab + (size_t)(k0 + 16 * kt + fr) * ng + c;
 #pragma unroll
     for (int t = 0; t < 9; ++t) *(f32x4*)(row + t * a.C) = acc[t][kt];
   }
+#endif
 }
 
 namespace {
@@ -553,7 +570,8 @@ struct D3WPlan {
 };
 bool plan_w(int N, int H, int W, int C, int K, D3WPlan* p) {
   if (g_direct == 0 || C % 64 || K % 64 || W < 8 || pow2_log(W) < 0) return false;
-  const int TW = W >= 64 ? 64 : W, TH = 64 / TW;  // 64-pixel chunks
+  // chunks of 128 pixels (64 for W = 8): a taller window amortises its halo rows
+  const int TW = W >= 64 ? 64 : W, TH = TW == 8 ? 8 : 128 / TW;
   if (H % TH) return false;
   if ((size_t)N * H * W * (C > K ? C : K) * 2 >= (1u << 31)) return false;
   p->TW = TW;
@@ -601,10 +619,10 @@ int conv3w_launch(const void* x, const void* dy, float* slab, size_t slab_bytes,
   *splits = p.splits;
   const dim3 grid(p.splits * p.ntiles), blk(256);
   switch (p.TW) {
-    case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<64, 1, 3>), grid, blk, 0, st, a); break;
-    case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<32, 2, 3>), grid, blk, 0, st, a); break;
-    case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<16, 4, 3>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3_wgrad_kernel<8, 8, 3>), grid, blk, 0, st, a); break;
+    case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<64, 2, 3>), grid, blk, 0, st, a); break;
+    case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<32, 4, 3>), grid, blk, 0, st, a); break;
+    case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<16, 8, 3>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3_wgrad_kernel<8, 8, 4>), grid, blk, 0, st, a); break;
   }
   SQR_HIP_LAUNCH_CHECK("conv3_wgrad_kernel");
   return 0;
