@@ -149,20 +149,22 @@ int sqr_conv2d_bwd_weight_col(const void* col, const void* dy, float* dw_kcrs, c
  * training != 0: batch statistics; save_mean/save_invstd [C] are written and running_mean/var
  *   (nullable) are updated as nn.BatchNorm2d does (momentum, unbiased running variance);
  * training == 0: normalises with running_mean/var.
- * y = relu?(gamma*(x-mean)*invstd + beta [+ residual]); residual nullable. */
+ * y = relu?(gamma*(x-mean)*invstd + beta [+ residual]); residual nullable.
+ * relu_mask (nullable, used only with relu): uint8 [M*C/8], bit k of byte i = (y[8i+k] > 0) of the
+ * stored values — what sqr_bn_bwd needs instead of re-reading y. */
 size_t sqr_bn_workspace_bytes(long long M, int C);
 int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const float* gamma, const float* beta,
                float* running_mean, float* running_var, float momentum, float eps, int training,
-               const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
+               const void* residual, int relu, void* y, uint8_t* relu_mask, float* save_mean, float* save_invstd,
                void* workspace, size_t workspace_bytes, void* stream);
 /* training-mode sqr_bn_fwd with the batch statistics taken from sqr_conv2d_fwd_stats partials */
 int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, const float* stats, int stats_rows,
                      const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
-                     float eps, const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
-                     void* workspace, size_t workspace_bytes, void* stream);
-/* backward of sqr_bn_fwd (training statistics): g = dy * [y > 0] (y = the forward output, NULL when
- * the forward had no ReLU); dx, dgamma = sum g*xhat, dbeta = sum g; dres (nullable) = g. */
-int sqr_bn_bwd(const void* dy, const void* y, const void* x, long long M, int C, int dtype, const float* gamma,
+                     float eps, const void* residual, int relu, void* y, uint8_t* relu_mask, float* save_mean,
+                     float* save_invstd, void* workspace, size_t workspace_bytes, void* stream);
+/* backward of sqr_bn_fwd (training statistics): g = dy * [y > 0] with the forward's relu_mask (NULL
+ * when the forward had no ReLU); dx, dgamma = sum g*xhat, dbeta = sum g; dres (nullable) = g. */
+int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* x, long long M, int C, int dtype, const float* gamma,
                const float* save_mean, const float* save_invstd, void* dx, void* dres, float* dgamma,
                float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 

@@ -61,9 +61,9 @@ __device__ __forceinline__ void load8f(const float* p, float* v) { V8<float>::lo
 // that 4 independent 16-B loads are in flight (the loop is otherwise latency-bound).
 template <typename T, int MODE>
 // MODE 0: a = x, b = x^2                                  (forward statistics)
-// MODE 1: g = dy*[y>0 if y]; a = g, b = g*(x - mean)      (backward)
+// MODE 1: g = dy*[relu bit]; a = g, b = g*(x - mean)     (backward; mask = NULL: no ReLU)
 __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                     const T* __restrict__ y, const float* __restrict__ mean,
+                                                     const uint8_t* __restrict__ mask, const float* __restrict__ mean,
                                                      int M, int C, int chunk, double* __restrict__ part) {
   extern __shared__ double red[];  // [rows][V][16]
   const int V = C >> 3, rows = 256 / V;
@@ -86,11 +86,10 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
         V8<T>::load(x + off, xv[u]);
         if (MODE == 1) {
           V8<T>::load(dy + off, g[u]);
-          if (y) {
-            float yv[8];
-            V8<T>::load(y + off, yv);
+          if (mask) {
+            const uint32_t mb = mask[off >> 3];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) g[u][i] = yv[i] > 0.f ? g[u][i] : 0.f;
+            for (int i = 0; i < 8; ++i) g[u][i] = (mb >> i) & 1 ? g[u][i] : 0.f;
           }
         }
       } else {
@@ -211,7 +210,7 @@ __global__ void infer_coef_kernel(int C, const float* __restrict__ gamma, const 
 template <typename T>
 __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                     const float* __restrict__ coef, int C, int nvec, int relu,
-                                                    T* __restrict__ y) {
+                                                    T* __restrict__ y, uint8_t* __restrict__ mask) {
   const int lv = __builtin_ctz(C >> 3);
   {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -235,6 +234,12 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
       for (int k = 0; k < 8; ++k) o[k] = fmaxf(o[k], 0.f);
     }
     V8<T>::store(y + i * 8, o);
+    if (mask) {  // ReLU mask of the STORED values, one bit per element: backward reads 1/16 of y
+      uint32_t mb = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mb |= (uint32_t)((float)(T)o[k] > 0.f) << k;
+      mask[i] = (uint8_t)mb;
+    }
   }
 }
 
@@ -258,9 +263,9 @@ __global__ void bwd_finalize_kernel(const double* __restrict__ part, int nblk, i
   coef[C + c] = (float)(-a * sg / M - k3 * mu);
 }
 
-// dx = k1*g + k3*x + k2 with g = dy*[y>0]; optionally dres = g
+// dx = k1*g + k3*x + k2 with g = dy*[relu bit]; optionally dres = g
 template <typename T>
-__global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                         const T* __restrict__ x, const float* __restrict__ coef,
                                                         int C, int nvec, T* __restrict__ dx,
                                                         T* __restrict__ dres) {
@@ -271,11 +276,10 @@ __global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy
     const int v = i & ((1 << lv) - 1);
     float g[8], xv[8], k1[8], k2[8], k3[8];
     V8<T>::load(dy + i * 8, g);
-    if (y) {
-      float yv[8];
-      V8<T>::load(y + i * 8, yv);
+    if (mask) {
+      const uint32_t mb = mask[i];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1 ? g[k] : 0.f;
     }
     V8<T>::load(x + i * 8, xv);
     load8f(coef + v * 8, k1);
@@ -547,7 +551,7 @@ extern "C" size_t sqr_bn_workspace_bytes(long long M, int C) {
 template <typename T>
 static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const float* beta, float* rmean,
                        float* rvar, float momentum, float eps, int training, const void* res, int relu, void* y,
-                       float* save_mean, float* save_invstd, void* ws, hipStream_t st, const float* ext = nullptr,
+                       uint8_t* mask, float* save_mean, float* save_invstd, void* ws, hipStream_t st, const float* ext = nullptr,
                        int ext_rows = 0) {
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
@@ -558,7 +562,7 @@ static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const fl
     SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel(ext)");
   } else if (training) {
     hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
-                       (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
+                       (const uint8_t*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("bn reduce_kernel");
     hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
@@ -570,15 +574,15 @@ static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const fl
   }
   const int nvec = M * (C / 8);
   hipLaunchKernelGGL((apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)x, (const T*)res, coef, C,
-                     nvec, relu, (T*)y);
+                     nvec, relu, (T*)y, relu ? mask : nullptr);
   SQR_HIP_LAUNCH_CHECK("bn apply_kernel");
   return 0;
 }
 
 extern "C" int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const float* gamma, const float* beta,
                           float* running_mean, float* running_var, float momentum, float eps, int training,
-                          const void* residual, int relu, void* y, float* save_mean, float* save_invstd,
-                          void* workspace, size_t workspace_bytes, void* stream) {
+                          const void* residual, int relu, void* y, uint8_t* relu_mask, float* save_mean,
+                          float* save_invstd, void* workspace, size_t workspace_bytes, void* stream) {
   int rc = check_mc(M, C, dtype);
   if (rc) return rc;
   SQR_CHECK_ARG(x && y && workspace, "bn_fwd: null pointer");
@@ -591,32 +595,32 @@ extern "C" int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const fl
   hipStream_t st = as_stream(stream);
   if (dtype == SQR_DTYPE_BF16)
     return bn_fwd_impl<bf16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training,
-                             residual, relu, y, save_mean, save_invstd, workspace, st);
+                             residual, relu, y, relu_mask, save_mean, save_invstd, workspace, st);
   return bn_fwd_impl<float>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training, residual,
-                            relu, y, save_mean, save_invstd, workspace, st);
+                            relu, y, relu_mask, save_mean, save_invstd, workspace, st);
 }
 
 template <typename T>
-static int bn_bwd_impl(const void* dy, const void* y, const void* x, int M, int C, const float* gamma,
+static int bn_bwd_impl(const void* dy, const uint8_t* mask, const void* x, int M, int C, const float* gamma,
                        const float* mean, const float* invstd, void* dx, void* dres, float* dgamma, float* dbeta,
                        void* ws, hipStream_t st) {
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
   hipLaunchKernelGGL((reduce_kernel<T, 1>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)dy,
-                     (const T*)y, mean, M, C, p.chunk, part);
+                     mask, mean, M, C, p.chunk, part);
   SQR_HIP_LAUNCH_CHECK("bn bwd reduce_kernel");
   hipLaunchKernelGGL(bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel");
   const int nvec = M * (C / 8);
-  hipLaunchKernelGGL((bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dy, (const T*)y,
+  hipLaunchKernelGGL((bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dy, mask,
                      (const T*)x, coef, C, nvec, (T*)dx, (T*)dres);
   SQR_HIP_LAUNCH_CHECK("bn bwd_apply_kernel");
   return 0;
 }
 
-extern "C" int sqr_bn_bwd(const void* dy, const void* y, const void* x, long long M, int C, int dtype,
+extern "C" int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* x, long long M, int C, int dtype,
                           const float* gamma, const float* save_mean, const float* save_invstd, void* dx, void* dres,
                           float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream) {
   int rc = check_mc(M, C, dtype);
@@ -628,10 +632,10 @@ extern "C" int sqr_bn_bwd(const void* dy, const void* y, const void* x, long lon
   }
   hipStream_t st = as_stream(stream);
   if (dtype == SQR_DTYPE_BF16)
-    return bn_bwd_impl<bf16>(dy, y, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, workspace,
-                             st);
-  return bn_bwd_impl<float>(dy, y, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta, workspace,
-                            st);
+    return bn_bwd_impl<bf16>(dy, relu_mask, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta,
+                             workspace, st);
+  return bn_bwd_impl<float>(dy, relu_mask, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta,
+                            workspace, st);
 }
 
 // ---------------------------------------------------------------- stem
@@ -654,7 +658,7 @@ static int stem_fwd_impl(const void* x, int N, int H, int W, int C, const float*
     SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel(ext)");
   } else if (training) {
     hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
-                       (const T*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
+                       (const uint8_t*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("stem reduce_kernel");
     hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
@@ -743,8 +747,9 @@ extern "C" int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t*
 // ---------------------------------------------------------------- with statistics from the conv epilogue
 extern "C" int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, const float* stats, int stats_rows,
                                 const float* gamma, const float* beta, float* running_mean, float* running_var,
-                                float momentum, float eps, const void* residual, int relu, void* y, float* save_mean,
-                                float* save_invstd, void* workspace, size_t workspace_bytes, void* stream) {
+                                float momentum, float eps, const void* residual, int relu, void* y, uint8_t* relu_mask,
+                                float* save_mean, float* save_invstd, void* workspace, size_t workspace_bytes,
+                                void* stream) {
   int rc = check_mc(M, C, dtype);
   if (rc) return rc;
   SQR_CHECK_ARG(x && y && stats && stats_rows > 0 && save_mean && save_invstd && workspace, "bn_fwd_stats: null pointer");
@@ -755,9 +760,9 @@ extern "C" int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, co
   hipStream_t st = as_stream(stream);
   if (dtype == SQR_DTYPE_BF16)
     return bn_fwd_impl<bf16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
-                             save_mean, save_invstd, workspace, st, stats, stats_rows);
+                             relu_mask, save_mean, save_invstd, workspace, st, stats, stats_rows);
   return bn_fwd_impl<float>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
-                            save_mean, save_invstd, workspace, st, stats, stats_rows);
+                            relu_mask, save_mean, save_invstd, workspace, st, stats, stats_rows);
 }
 
 extern "C" int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int dtype, const float* stats,

@@ -59,12 +59,12 @@ SIGNATURES = {
     "sqr_bn_workspace_bytes": (c_size_t, [ctypes.c_longlong, c_int]),
     "sqr_bn_fwd": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_float, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_size_t, c_void_p]),
+                           c_void_p, c_size_t, c_void_p]),
     "sqr_bn_bwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_bn_fwd_stats": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_float, c_float, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                                 c_void_p, c_size_t, c_void_p]),
+                                 c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_stem_fwd_stats": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),

@@ -45,6 +45,8 @@ class BNActFn(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=x.device)
         mean = torch.empty(C, **f32)
         invstd = torch.empty(C, **f32)
+        # ReLU mask (1 bit per element) for the backward instead of keeping/reading y
+        mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if (relu and training) else None
         n = _ws_bytes(M, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         rm = ptr(rmean) if rmean is not None else ctypes.c_void_p(0)
@@ -52,29 +54,29 @@ class BNActFn(torch.autograd.Function):
         if training and stats is not None:  # batch statistics from the producing conv's epilogue
             check(lib().sqr_bn_fwd_stats(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(stats), stats.shape[0],
                                          ptr(weight), ptr(bias), rm, rv, ctypes.c_float(momentum),
-                                         ctypes.c_float(eps), ptr(residual), int(relu), ptr(y), ptr(mean),
+                                         ctypes.c_float(eps), ptr(residual), int(relu), ptr(y), ptr(mask), ptr(mean),
                                          ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_bn_fwd_stats")
         else:
             check(lib().sqr_bn_fwd(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(bias), rm, rv,
                                    ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(residual),
-                                   int(relu), ptr(y), ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)),
-                  "sqr_bn_fwd")
+                                   int(relu), ptr(y), ptr(mask), ptr(mean), ptr(invstd), ptr(ws), n,
+                                   stream_ptr(x.device)), "sqr_bn_fwd")
         ctx.relu, ctx.training, ctx.eps = relu, training, eps
         ctx.has_res = residual is not None
         if training:
-            ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+            ctx.save_for_backward(x, mask, weight, mean, invstd)
         else:
             ctx.save_for_backward(x, y if relu else None, weight, rmean.clone(), rvar.clone())
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, m, v = ctx.saved_tensors
+        x, ym, weight, m, v = ctx.saved_tensors  # ym: ReLU mask (training) or y (eval)
         dy = dy.to(x.dtype).contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
         if not ctx.training:  # eval-mode backward (running statistics are constants): plain torch
-            g = dy.float() * (y > 0) if y is not None else dy.float()
+            g = dy.float() * (ym > 0) if ym is not None else dy.float()
             invstd = torch.rsqrt(v + ctx.eps)
             xhat = (x.float() - m.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
             dx = (g * (weight * invstd).view(1, C, 1, 1)).to(x.dtype)
@@ -86,7 +88,7 @@ class BNActFn(torch.autograd.Function):
         dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
         n = _ws_bytes(M, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(lib().sqr_bn_bwd(ptr(dy), ptr(y), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
+        check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
         if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
