@@ -134,5 +134,14 @@ class ResNetSQ(nn.Module):
         x = self.encoder(_cl(x))  # fp32 features (the encoder's MLP tail runs in fp32)
         with torch.autocast("cuda", enabled=False):
             x = x.float()
-            return (self.output_size.forward(x), self.output_shape.forward(x), self.output_position.forward(x),
-                    self.output_rotation.forward(x))
+            heads = (self.output_size, self.output_shape, self.output_position, self.output_rotation)
+            if any(h.dense for h in heads):
+                return tuple(h.forward(x) for h in heads)
+            # the four 256->n heads as ONE 256->12 GEMM (same parameters / state-dict keys):
+            # z = [a | e | t | q] pre-activations, sigmoid on the first 8, L2-normalised quaternion
+            w = torch.cat([h.out_layer[0].weight for h in heads])
+            b = torch.cat([h.out_layer[0].bias for h in heads])
+            z = torch.nn.functional.linear(x, w, b)
+            s = torch.sigmoid(z[:, :8])
+            q = z[:, 8:]
+            return s[:, :3], s[:, 3:5], s[:, 5:8], q / torch.norm(q, 2, -1, keepdim=True)
