@@ -25,6 +25,7 @@
  *   sqr_bn_fwd / sqr_bn_bwd    torch.nn.BatchNorm2d (+ residual add + ReLU) of torchvision resnet18's
  *                              BasicBlock (ResNetSQ encoder, torch/models.py:181), training and eval.
  *   sqr_stem_fwd / _bwd        resnet18 stem bn1 -> relu -> maxpool(3,2,1) (torch/models.py:181).
+ *   sqr_tail_fwd / _bwd        ResNetSQ avgpool + encoder.fc + output heads (torch/models.py:7-99,186-204).
  */
 #ifndef SQR_H
 #define SQR_H
@@ -48,6 +49,12 @@ extern "C" {
 
 int sqr_version(void);
 const char* sqr_last_error_string(void);
+
+/* Measurement hook (bench.py): arm two hipEvent_t (passed as void*) to be recorded on the launch
+ * stream immediately before and after the NEXT main conv kernel (the implicit-GEMM / direct
+ * kernel of a sqr_conv2d_* call, not its im2col / split-K reduction launches); the hook then
+ * disarms itself.  NULL, NULL disarms.  Per calling thread. */
+int sqr_probe_arm(void* start_event, void* stop_event);
 
 /* ---------------------------------------------------------------- losses */
 
@@ -183,6 +190,36 @@ int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int dtype, con
 int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t* argmax, const void* x, int N, int H, int W,
                  int C, int dtype, const float* gamma, const float* save_mean, const float* save_invstd, void* dx,
                  float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- ResNetSQ tail (fused) */
+
+/* adaptive avg-pool + encoder.fc (Linear-LeakyReLU-Linear-LeakyReLU) + the 4 heads of ResNetSQ
+ * (torch/models.py:186-204, heads :7-99): x [B][P][C0] (NHWC layer-4 output, P = H*W pixels, dtype)
+ * -> a [B,3], e [B,2], t [B,3] (sigmoid), q [B,4] (L2-normalised), all f32.  Parameters are the
+ * fp32 nn.Linear weights [out][in] / biases.  Constraints: C0 a power of 2 <= 1024, F1, F2
+ * multiples of 4 <= 1024. */
+typedef struct sqr_tail_desc {
+  int B, P, C0, F1, F2, dtype;
+  const float *w0, *b0;   /* encoder.fc.0: [F1][C0], [F1] */
+  const float *w1, *b1;   /* encoder.fc.2: [F2][F1], [F2] */
+  const float* wh[4];     /* output_{size,shape,position,rotation}.out_layer.0.weight [3|2|3|4][F2] */
+  const float* bh[4];
+} sqr_tail_desc;
+/* save: sqr_tail_save_floats(t) floats written by the forward, read by the backward */
+size_t sqr_tail_save_floats(const sqr_tail_desc* t);
+int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a, float* out_e, float* out_t, float* out_q,
+                 float* save, void* stream);
+typedef struct sqr_tail_grads {
+  const float* g_out[4];  /* upstream grads of a, e, t, q: rows of ld[h] floats; NULL = zero */
+  int ld[4];
+  void* dx;               /* [B][P][C0] dtype: d loss / d x */
+  float *dw0, *db0, *dw1, *db1;
+  float* dwh[4];
+  float* dbh[4];
+} sqr_tail_grads;
+size_t sqr_tail_workspace_bytes(const sqr_tail_desc* t);
+int sqr_tail_bwd(const sqr_tail_desc* t, const float* save, const sqr_tail_grads* g, void* workspace,
+                 size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

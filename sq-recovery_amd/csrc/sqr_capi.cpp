@@ -12,7 +12,28 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+// one-shot kernel probe: events recorded on the launch stream around the next main conv kernel
+static thread_local hipEvent_t g_probe_start = nullptr, g_probe_stop = nullptr;
+
+void probe_begin(hipStream_t st) {
+  if (g_probe_start) (void)hipEventRecord(g_probe_start, st);
+}
+
+void probe_end(hipStream_t st) {
+  if (g_probe_start) {
+    (void)hipEventRecord(g_probe_stop, st);
+    g_probe_start = g_probe_stop = nullptr;
+  }
+}
 }  // namespace sqr
 
 extern "C" int sqr_version(void) { return 1; }
 extern "C" const char* sqr_last_error_string(void) { return sqr::g_err; }
+
+extern "C" int sqr_probe_arm(void* start_event, void* stop_event) {
+  SQR_CHECK_ARG((start_event == nullptr) == (stop_event == nullptr), "probe_arm: give both events or neither");
+  sqr::g_probe_start = (hipEvent_t)start_event;
+  sqr::g_probe_stop = (hipEvent_t)stop_event;
+  return 0;
+}

@@ -9,6 +9,9 @@
 namespace sqr {
 
 void set_error(const char* fmt, ...);
+// sqr_probe_arm: record the armed events around the next main conv kernel launch (then disarm)
+void probe_begin(hipStream_t st);
+void probe_end(hipStream_t st);
 
 #define SQR_CHECK_ARG(cond, ...)            \
   do {                                      \

@@ -55,6 +55,14 @@ struct NTArgs {
   float* stats;    // nullable: per-M-tile BatchNorm partials [ntm][2][Nout] (sum, sum of squares)
 };
 
+// up to 4 independent NT GEMMs in one launch (the stride-parity classes of a strided dgrad):
+// blocks [start[i], start[i+1]) of the XCD-remapped id space run class i
+struct NTMulti {
+  NTArgs c[4];
+  int start[4];
+  int ncls;
+};
+
 struct TNArgs {
   Gather g;          // P operand: X gathered, [pixels][Ng], Ng = R*S*Ci
   const void* dy;    // Q operand: dY [pixels][Kout]
@@ -80,7 +88,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_row_block) {
 // tiles kt+1..kt+STAGES-1 stay in flight across the raw s_barrier; a counted s_waitcnt vmcnt
 // retires exactly the tile read next.
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
-__global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
+__global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
   using C = Cfg<T>;
   constexpr int BK = 128 / C::ES;  // k elements per LDS row (128 B)
   constexpr int ROWB = 128;
@@ -95,11 +103,16 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTArgs a) {
   // the tap table lived in LDS) — tap -> (r, s) is computed with a multiply-high instead.
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
 
-  const Gather& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid_all = xcd_remap(blockIdx.x, gridDim.x);
+  const int cls = mc.ncls == 1 ? 0
+                               : (int)(bid_all >= mc.start[1]) + (int)(mc.ncls > 2 && bid_all >= mc.start[2]) +
+                                     (int)(mc.ncls > 3 && bid_all >= mc.start[3]);
+  const NTArgs& a = mc.c[cls];
+  const int bid = bid_all - mc.start[cls];
+  const Gather& g = a.g;
   const int tile_m = bid / a.ntn, tile_n = bid % a.ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
@@ -811,21 +824,35 @@ int nt_cfg(int M, int N) {
   return 3;
 }
 
+// one launch for ncls NT GEMMs of the same output width (tile config from their total M)
 template <typename T>
-int launch_nt(NTArgs a, hipStream_t st) {
+int launch_nt(NTArgs* cl, int ncls, hipStream_t st) {
   // tile choice: biggest tile that still gives >= 2 workgroups per CU (512), else the smallest
-  const int M = a.g.M, N = a.Nout;
+  int M = 0;
+  for (int i = 0; i < ncls; ++i) M += cl[i].g.M;
+  const int N = cl[0].Nout;
   const int cfg = nt_cfg(M, N);
   int bm = (cfg == 0 || cfg == 1) ? 128 : 64, bn = (cfg == 0 || cfg == 2) ? 128 : 64;
-  a.ntm = (M + bm - 1) / bm;
-  a.ntn = (N + bn - 1) / bn;
-  const dim3 grid(a.ntm * a.ntn), blk(256);
-  switch (cfg) {
-    case 0: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, a); break;
-    case 1: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, a); break;
+  NTMulti mc;
+  int total = 0;
+  for (int i = 0; i < ncls; ++i) {
+    cl[i].ntm = (cl[i].g.M + bm - 1) / bm;
+    cl[i].ntn = (N + bn - 1) / bn;
+    mc.c[i] = cl[i];
+    mc.start[i] = total;
+    total += cl[i].ntm * cl[i].ntn;
   }
+  for (int i = ncls; i < 4; ++i) mc.start[i] = total;
+  mc.ncls = ncls;
+  const dim3 grid(total), blk(256);
+  probe_begin(st);
+  switch (cfg) {
+    case 0: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, mc); break;
+    case 1: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, mc); break;
+    case 2: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, mc); break;
+    default: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, mc); break;
+  }
+  probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv_nt_kernel");
   return 0;
 }
@@ -858,10 +885,12 @@ int launch_tn(TNArgs a, const TNPlan& p, hipStream_t st) {
   a.ntn = p.ntn;
   a.kchunk = p.kchunk;
   const dim3 grid(p.ntm * p.ntn * p.splits), blk(256);
+  probe_begin(st);
   if (p.bm == 128 && p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, a);
   else if (p.bm == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, a);
   else if (p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, a);
   else hipLaunchKernelGGL((conv_tn_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, a);
+  probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv_tn_kernel");
   return 0;
 }
@@ -967,7 +996,7 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
     a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, -d->pad, 1, d->R, d->S, d->N, sh.ES);
     a.Kg = d->R * d->S * d->C;
   }
-  return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
+  return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(&a, 1, st) : launch_nt<float>(&a, 1, st);
 }
 
 extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d,
@@ -1023,11 +1052,14 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
   // Output pixels split by parity (h%st, w%st); in class (ph,pw) only taps r = r0 + st*t contribute
   // and dY row = i + off_h - t: a stride-1 implicit GEMM over the class grid (Hc x Wc).
   const char* wp = (const char*)w_crsk;
+  NTArgs cl[4];
+  int ncls = 0;
   for (int ph = 0; ph < d->stride; ++ph) {
     for (int pw = 0; pw < d->stride; ++pw) {
       const DgradClass c = dgrad_class(d, ph, pw);
       if (c.Hc == 0 || c.Wc == 0) continue;
-      NTArgs a;
+      SQR_CHECK_ARG(ncls < 4, "conv2d_bwd_data: stride %d > 2 not supported", d->stride);
+      NTArgs& a = cl[ncls++];
       a.g = make_gather(dy, sh.Ho, sh.Wo, d->K, c.Hc, c.Wc, 1, c.off_h, c.off_w, -1, c.Rc > 0 ? c.Rc : 1,
                         c.Sc > 0 ? c.Sc : 1, d->N, sh.ES);
       a.w = wp;
@@ -1040,12 +1072,11 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
       a.opw = pw;
       a.oH = d->H;
       a.oW = d->W;
-      rc = d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(a, st) : launch_nt<float>(a, st);
-      if (rc) return rc;
       wp += (size_t)d->C * c.Rc * c.Sc * d->K * sh.ES;
     }
   }
-  return 0;
+  if (ncls == 0) return 0;
+  return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(cl, ncls, st) : launch_nt<float>(cl, ncls, st);
 }
 
 static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, float* dw_kcrs,

@@ -553,12 +553,14 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
   a.wbytes = (uint32_t)wbytes;
   if (stats_rows) *stats_rows = a.ntm;
   const dim3 grid(a.ntm * a.ntn), blk(c.threads);
+  probe_begin(st);
   switch (c.id) {
     case 0: hipLaunchKernelGGL((conv3_kernel<256, 64, 4, 1, 64, 4, 1>), grid, blk, 0, st, a); break;
     case 1: hipLaunchKernelGGL((conv3_kernel<256, 128, 4, 2, 32, 8, 2>), grid, blk, 0, st, a); break;
     case 2: hipLaunchKernelGGL((conv3_kernel<128, 128, 4, 2, 16, 8, 2>), grid, blk, 0, st, a); break;
     default: hipLaunchKernelGGL((conv3_kernel<64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
   }
+  probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_kernel");
   return 0;
 }
@@ -618,12 +620,14 @@ int conv3w_launch(const void* x, const void* dy, float* slab, size_t slab_bytes,
   a.dybytes = (uint32_t)((size_t)N * H * W * K * 2);
   *splits = p.splits;
   const dim3 grid(p.splits * p.ntiles), blk(256);
+  probe_begin(st);
   switch (p.TW) {
     case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<64, 2, 3>), grid, blk, 0, st, a); break;
     case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<32, 4, 3>), grid, blk, 0, st, a); break;
     case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<16, 8, 3>), grid, blk, 0, st, a); break;
     default: hipLaunchKernelGGL((conv3_wgrad_kernel<8, 8, 4>), grid, blk, 0, st, a); break;
   }
+  probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_wgrad_kernel");
   return 0;
 }

@@ -1,0 +1,426 @@
+// ResNetSQ regression tail: adaptive average pool + encoder.fc (Linear-LeakyReLU-Linear-LeakyReLU)
+// + the four output heads (torch/models.py:186-204; heads :7-99), forward as ONE kernel and
+// backward as two.  The tail holds ~0.2 M parameters and B x 512 features: in stock PyTorch it is
+// ~40 small GEMM / elementwise / reduction launches per training step, each paying a kernel
+// boundary; here it is three launches, all fp32 (the layer-4 activation may be bf16).
+//
+//   forward   grid B (one workgroup per sample):
+//     feat = mean_p x[n][p][:]          (x: the layer-4 output, NHWC [B][P][C0])
+//     h0 = leaky(W0 feat + b0)           (encoder.fc.0 / .1, LeakyReLU slope 0.01)
+//     h1 = leaky(W1 h0 + b1)             (encoder.fc.2 / .3)
+//     z  = Wh h1 + bh                    (output_{size,shape,position,rotation}.out_layer.0)
+//     a, e, t = sigmoid(z[0:3]), sigmoid(z[3:5]), sigmoid(z[5:8]);  q = z[8:12] / |z[8:12]|
+//     saved per sample: feat, pre-activations of h0 and h1, z
+//   backward  grid B: dz (sigmoid' / normalisation Jacobian), d1 = (Wh^T dz) * leaky'(h1),
+//     d0 = (W1^T d1) * leaky'(h0), dx[n][p][:] = (W0^T d0) / P  (mean backward, broadcast)
+//   weights   grid rows/4: dW = sum_n d[n] (x) act[n], db = sum_n d[n], samples in a fixed order
+// Dot products over a weight row are wave-cooperative (coalesced rows, fixed xor-tree order);
+// transposed products (W^T d) split the reduction over the 4 waves and add the 4 parts in order.
+// Every sum has a fixed order: results are bitwise reproducible.
+#include <stdint.h>
+#include "sqr_common.h"
+
+namespace sqr {
+namespace tail {
+
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int MAXF = 1024;  // max features of any tail layer (C0, F1, F2)
+constexpr int NOUT = 12;     // a(3) e(2) t(3) q(4)
+
+struct Dev {
+  int B, P, C0, F1, F2, ldsave;
+  const void* x;
+  const float *w0, *b0, *w1, *b1;
+  const float* wh[4];
+  const float* bh[4];
+};
+
+__device__ __forceinline__ int head_of(int i) { return i < 3 ? 0 : (i < 5 ? 1 : (i < 8 ? 2 : 3)); }
+__device__ __forceinline__ int head_row(int i) { return i < 3 ? i : (i < 5 ? i - 3 : (i < 8 ? i - 5 : i - 8)); }
+__device__ __forceinline__ float leaky(float v) { return v > 0.f ? v : v * 0.01f; }
+__device__ __forceinline__ float leaky_grad(float pre, float g) { return pre > 0.f ? g : g * 0.01f; }
+__device__ __forceinline__ float sigmoidf(float z) { return 1.f / (1.f + expf(-z)); }
+
+template <typename T> struct IO;
+template <> struct IO<bf16> {
+  static __device__ __forceinline__ void load8(const bf16* p, float* v) {
+    const u32x4 u = *(const u32x4*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store8(bf16* p, const float* v) {
+    typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+    *(bf16x8*)p = o;
+  }
+};
+template <> struct IO<float> {
+  static __device__ __forceinline__ void load8(const float* p, float* v) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[4 + i] = b[i];
+    }
+  }
+  static __device__ __forceinline__ void store8(float* p, const float* v) {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+};
+
+// one wave: dot(w[0..n), v[0..n)), n % 4 == 0, v in LDS; lanes stride 4 floats, xor-tree sum
+__device__ __forceinline__ float wave_dot(const float* __restrict__ w, const float* v, int n, int lane) {
+  float s = 0.f;
+  for (int c = lane * 4; c < n; c += 256) {
+    const f32x4 a = *(const f32x4*)(w + c);
+    s = fmaf(a[0], v[c], s);
+    s = fmaf(a[1], v[c + 1], s);
+    s = fmaf(a[2], v[c + 2], s);
+    s = fmaf(a[3], v[c + 3], s);
+  }
+  return wave_sum(s);
+}
+
+// y = W x over rows [0, rows): wave w takes rows w, w+4, ... (4 rows in flight per iteration)
+__device__ __forceinline__ void rows_dot(const float* __restrict__ W, const float* __restrict__ bias, const float* v,
+                                         int rows, int n, int wave, int lane, float* pre_out, float* act_out) {
+  for (int j = wave; j < rows; j += 16) {
+    float s[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = j + 4 * u;
+      s[u] = r < rows ? wave_dot(W + (size_t)r * n, v, n, lane) : 0.f;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = j + 4 * u;
+        if (r < rows) {
+          const float p = s[u] + bias[r];
+          pre_out[r] = p;
+          act_out[r] = leaky(p);
+        }
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict__ save, float* __restrict__ out_a,
+                                                       float* __restrict__ out_e, float* __restrict__ out_t,
+                                                       float* __restrict__ out_q) {
+  __shared__ float feat[MAXF], h0[MAXF], h1[MAXF], red[2048], z[16];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* sv = save + (size_t)n * d.ldsave;
+
+  // average pool: thread = (pixel phase, 8-channel vector); phases * C0 == 2048
+  const int V = d.C0 >> 3, phases = 256 / V;
+  const int v = tid % V, ph = tid / V;
+  {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const T* xn = (const T*)d.x + (size_t)n * d.P * d.C0 + v * 8;
+    for (int p = ph; p < d.P; p += phases) {
+      float t[8];
+      IO<T>::load8(xn + (size_t)p * d.C0, t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += t[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[ph * d.C0 + v * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < d.C0; c += 256) {
+    float s = 0.f;
+    for (int q = 0; q < phases; ++q) s += red[q * d.C0 + c];
+    s = s / (float)d.P;
+    feat[c] = s;
+    sv[c] = s;
+  }
+  __syncthreads();
+  rows_dot(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
+  __syncthreads();
+  rows_dot(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
+  __syncthreads();
+  for (int i = wave; i < NOUT; i += 4) {
+    const int hd = head_of(i), r = head_row(i);
+    const float s = wave_dot(d.wh[hd] + (size_t)r * d.F2, h1, d.F2, lane) + d.bh[hd][r];
+    if (lane == 0) {
+      z[i] = s;
+      sv[d.C0 + d.F1 + d.F2 + i] = s;
+    }
+  }
+  __syncthreads();
+  if (tid < NOUT) {
+    const float zi = z[tid];
+    if (tid < 3) out_a[n * 3 + tid] = sigmoidf(zi);
+    else if (tid < 5) out_e[n * 2 + tid - 3] = sigmoidf(zi);
+    else if (tid < 8) out_t[n * 3 + tid - 5] = sigmoidf(zi);
+    else {
+      const float nrm = sqrtf(z[8] * z[8] + z[9] * z[9] + z[10] * z[10] + z[11] * z[11]);
+      out_q[n * 4 + tid - 8] = zi / nrm;
+    }
+  }
+}
+
+struct Up {  // upstream gradients of a, e, t, q (nullable = zero) and their row strides
+  const float* g[4];
+  int ld[4];
+};
+
+// grad of one output element (0 if that output received no gradient)
+__device__ __forceinline__ float up_grad(const Up& u, int n, int i) {
+  const int hd = head_of(i), r = head_row(i);
+  const float* g = u.g[hd];
+  return g ? g[(size_t)n * u.ld[hd] + r] : 0.f;
+}
+
+// out[j] = sum_k in[k] * W[k][j] for j < ncols, k < nrows: lanes own 4 columns each (float4 rows
+// reads), the 4 waves split k and their partial sums are added in wave order through LDS
+__device__ __forceinline__ void cols_dot(const float* __restrict__ W, const float* in, int nrows, int ncols,
+                                         int wave, int lane, float* part /*[4][MAXF]*/) {
+  const int kper = (nrows + 3) / 4, k0 = wave * kper, k1 = min(nrows, k0 + kper);
+  for (int c = lane * 4; c < ncols; c += 256) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int k = k0; k < k1; ++k) {
+      const f32x4 w = *(const f32x4*)(W + (size_t)k * ncols + c);
+      const float g = in[k];
+      s[0] = fmaf(g, w[0], s[0]);
+      s[1] = fmaf(g, w[1], s[1]);
+      s[2] = fmaf(g, w[2], s[2]);
+      s[3] = fmaf(g, w[3], s[3]);
+    }
+    *(f32x4*)(part + wave * MAXF + c) = s;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) tail_bwd_kernel(Dev d, const float* __restrict__ save, Up up,
+                                                       T* __restrict__ dx, float* __restrict__ dsave) {
+  __shared__ float g0[MAXF], g1[MAXF], part[4 * MAXF], dz[16];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* sv = save + (size_t)n * d.ldsave;
+  const float* pre0 = sv + d.C0;
+  const float* pre1 = pre0 + d.F1;
+  const float* zs = pre1 + d.F2;
+  const int ldd = d.F1 + d.F2 + NOUT;
+  float* ds = dsave + (size_t)n * ldd;  // [d0 F1][d1 F2][dz 12]
+
+  if (tid < NOUT) {
+    const float gi = up_grad(up, n, tid), zi = zs[tid];
+    float r;
+    if (tid < 8) {
+      const float s = sigmoidf(zi);
+      r = gi * (1.f - s) * s;
+    } else {
+      // q = z / |z|:  dz = (g - q (q . g)) / |z|
+      const float nrm = sqrtf(zs[8] * zs[8] + zs[9] * zs[9] + zs[10] * zs[10] + zs[11] * zs[11]);
+      float dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dot = fmaf(up_grad(up, n, 8 + k), zs[8 + k] / nrm, dot);
+      r = (gi - (zi / nrm) * dot) / nrm;
+    }
+    dz[tid] = r;
+    ds[d.F1 + d.F2 + tid] = r;
+  }
+  __syncthreads();
+  for (int k = tid; k < d.F2; k += 256) {  // dh1 = Wh^T dz (12 rows)
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) s = fmaf(dz[i], d.wh[head_of(i)][(size_t)head_row(i) * d.F2 + k], s);
+    const float g = leaky_grad(pre1[k], s);
+    g1[k] = g;
+    ds[d.F1 + k] = g;
+  }
+  __syncthreads();
+  cols_dot(d.w1, g1, d.F2, d.F1, wave, lane, part);  // dh0 = W1^T d1
+  __syncthreads();
+  for (int j = tid; j < d.F1; j += 256) {
+    const float s = ((part[j] + part[MAXF + j]) + part[2 * MAXF + j]) + part[3 * MAXF + j];
+    const float g = leaky_grad(pre0[j], s);
+    g0[j] = g;
+    ds[j] = g;
+  }
+  __syncthreads();
+  cols_dot(d.w0, g0, d.F1, d.C0, wave, lane, part);  // dfeat = W0^T d0
+  __syncthreads();
+  for (int c = tid; c < d.C0; c += 256) {
+    const float s = ((part[c] + part[MAXF + c]) + part[2 * MAXF + c]) + part[3 * MAXF + c];
+    g1[c] = s / (float)d.P;  // mean backward: dfeat / P on every pixel (g1 reused)
+  }
+  __syncthreads();
+  const int V = d.C0 >> 3;
+  T* dxn = dx + (size_t)n * d.P * d.C0;
+  for (int i = tid; i < d.P * V; i += 256) {
+    const int v = i % V;
+    IO<T>::store8(dxn + (size_t)i * 8, g1 + v * 8);
+  }
+}
+
+struct WOut {
+  float *dw0, *db0, *dw1, *db1;
+  float* dwh[4];
+  float* dbh[4];
+};
+
+// 4 weight rows per block: section 0 = fc.0 rows (act = feat), 1 = fc.2 rows (act = leaky(pre0)),
+// 2 = head rows (act = leaky(pre1)).  dW[r][c] = sum_n d[n][r] act[n][c] in sample order.
+__global__ void __launch_bounds__(256) tail_wgrad_kernel(Dev d, const float* __restrict__ save,
+                                                         const float* __restrict__ dsave, WOut o) {
+  const int b0n = d.F1 / 4, b1n = d.F2 / 4;
+  int sec, r0;
+  if ((int)blockIdx.x < b0n) {
+    sec = 0;
+    r0 = blockIdx.x * 4;
+  } else if ((int)blockIdx.x < b0n + b1n) {
+    sec = 1;
+    r0 = (blockIdx.x - b0n) * 4;
+  } else {
+    sec = 2;
+    r0 = (blockIdx.x - b0n - b1n) * 4;
+  }
+  const int ncols = sec == 0 ? d.C0 : (sec == 1 ? d.F1 : d.F2);
+  const int aoff = sec == 0 ? 0 : (sec == 1 ? d.C0 : d.C0 + d.F1);        // activation in save
+  const int doff = sec == 0 ? 0 : (sec == 1 ? d.F1 : d.F1 + d.F2);        // d in dsave
+  const int ldd = d.F1 + d.F2 + NOUT;
+  for (int c = threadIdx.x; c < ncols; c += 256) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < d.B; ++n) {
+      float a = save[(size_t)n * d.ldsave + aoff + c];
+      if (sec > 0) a = leaky(a);
+      const float* dn = dsave + (size_t)n * ldd + doff + r0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] = fmaf(dn[u], a, acc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + u;
+      if (sec == 0) o.dw0[(size_t)r * ncols + c] = acc[u];
+      else if (sec == 1) o.dw1[(size_t)r * ncols + c] = acc[u];
+      else o.dwh[head_of(r)][(size_t)head_row(r) * ncols + c] = acc[u];
+    }
+  }
+  if (threadIdx.x < 4) {
+    const int r = r0 + threadIdx.x;
+    float s = 0.f;
+    for (int n = 0; n < d.B; ++n) s += dsave[(size_t)n * ldd + doff + r];
+    if (sec == 0) o.db0[r] = s;
+    else if (sec == 1) o.db1[r] = s;
+    else o.dbh[head_of(r)][head_row(r)] = s;
+  }
+}
+
+}  // namespace tail
+}  // namespace sqr
+
+using namespace sqr;
+using namespace sqr::tail;
+
+namespace {
+int check_tail(const sqr_tail_desc* t) {
+  SQR_CHECK_ARG(t, "tail: null descriptor");
+  SQR_CHECK_ARG(t->B >= 1 && t->B <= 65535 && t->P >= 1, "tail: bad B=%d P=%d", t->B, t->P);
+  SQR_CHECK_ARG(t->C0 >= 8 && t->C0 <= MAXF && (t->C0 & (t->C0 - 1)) == 0, "tail: C0=%d must be a power of 2 in [8, %d]",
+                t->C0, MAXF);
+  SQR_CHECK_ARG(t->F1 >= 4 && t->F1 <= MAXF && t->F1 % 4 == 0 && t->F2 >= 4 && t->F2 <= MAXF && t->F2 % 4 == 0,
+                "tail: F1=%d F2=%d must be multiples of 4 in [4, %d]", t->F1, t->F2, MAXF);
+  SQR_CHECK_ARG(t->dtype == SQR_DTYPE_F32 || t->dtype == SQR_DTYPE_BF16, "tail: bad dtype");
+  SQR_CHECK_ARG(t->w0 && t->b0 && t->w1 && t->b1, "tail: null fc parameter");
+  for (int h = 0; h < 4; ++h) SQR_CHECK_ARG(t->wh[h] && t->bh[h], "tail: null head %d parameter", h);
+  SQR_CHECK_ARG((size_t)t->B * t->P * t->C0 < (1ull << 31), "tail: activation too large");
+  return 0;
+}
+
+Dev make_dev(const sqr_tail_desc* t, const void* x) {
+  Dev d;
+  d.B = t->B;
+  d.P = t->P;
+  d.C0 = t->C0;
+  d.F1 = t->F1;
+  d.F2 = t->F2;
+  d.ldsave = t->C0 + t->F1 + t->F2 + NOUT;
+  d.x = x;
+  d.w0 = t->w0;
+  d.b0 = t->b0;
+  d.w1 = t->w1;
+  d.b1 = t->b1;
+  for (int h = 0; h < 4; ++h) {
+    d.wh[h] = t->wh[h];
+    d.bh[h] = t->bh[h];
+  }
+  return d;
+}
+}  // namespace
+
+extern "C" size_t sqr_tail_save_floats(const sqr_tail_desc* t) {
+  if (check_tail(t)) return 0;
+  return (size_t)t->B * (t->C0 + t->F1 + t->F2 + NOUT);
+}
+
+extern "C" size_t sqr_tail_workspace_bytes(const sqr_tail_desc* t) {
+  if (check_tail(t)) return 0;
+  return (size_t)t->B * (t->F1 + t->F2 + NOUT) * sizeof(float);
+}
+
+extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a, float* out_e, float* out_t,
+                            float* out_q, float* save, void* stream) {
+  int rc = check_tail(t);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && out_a && out_e && out_t && out_q && save, "tail_fwd: null pointer");
+  const Dev d = make_dev(t, x);
+  hipStream_t st = as_stream(stream);
+  if (t->dtype == SQR_DTYPE_BF16)
+    hipLaunchKernelGGL(tail_fwd_kernel<bf16>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
+  else
+    hipLaunchKernelGGL(tail_fwd_kernel<float>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
+  SQR_HIP_LAUNCH_CHECK("tail_fwd_kernel");
+  return 0;
+}
+
+extern "C" int sqr_tail_bwd(const sqr_tail_desc* t, const float* save, const sqr_tail_grads* g, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+  int rc = check_tail(t);
+  if (rc) return rc;
+  SQR_CHECK_ARG(save && g && workspace, "tail_bwd: null pointer");
+  SQR_CHECK_ARG(g->dx && g->dw0 && g->db0 && g->dw1 && g->db1, "tail_bwd: null gradient output");
+  for (int h = 0; h < 4; ++h) {
+    SQR_CHECK_ARG(g->dwh[h] && g->dbh[h], "tail_bwd: null head %d gradient output", h);
+    SQR_CHECK_ARG(!g->g_out[h] || g->ld[h] >= (h == 1 ? 2 : (h == 3 ? 4 : 3)), "tail_bwd: bad ld[%d]=%d", h, g->ld[h]);
+  }
+  if (workspace_bytes < sqr_tail_workspace_bytes(t)) {
+    set_error("tail_bwd: workspace %zu < %zu bytes", workspace_bytes, sqr_tail_workspace_bytes(t));
+    return SQR_E_WORKSPACE;
+  }
+  const Dev d = make_dev(t, nullptr);
+  Up up;
+  WOut o;
+  for (int h = 0; h < 4; ++h) {
+    up.g[h] = g->g_out[h];
+    up.ld[h] = g->ld[h];
+    o.dwh[h] = g->dwh[h];
+    o.dbh[h] = g->dbh[h];
+  }
+  o.dw0 = g->dw0;
+  o.db0 = g->db0;
+  o.dw1 = g->dw1;
+  o.db1 = g->db1;
+  float* dsave = (float*)workspace;
+  hipStream_t st = as_stream(stream);
+  if (t->dtype == SQR_DTYPE_BF16)
+    hipLaunchKernelGGL(tail_bwd_kernel<bf16>, dim3(t->B), dim3(256), 0, st, d, save, up, (bf16*)g->dx, dsave);
+  else
+    hipLaunchKernelGGL(tail_bwd_kernel<float>, dim3(t->B), dim3(256), 0, st, d, save, up, (float*)g->dx, dsave);
+  SQR_HIP_LAUNCH_CHECK("tail_bwd_kernel");
+  const int blocks = t->F1 / 4 + t->F2 / 4 + NOUT / 4;
+  hipLaunchKernelGGL(tail_wgrad_kernel, dim3(blocks), dim3(256), 0, st, d, save, (const float*)dsave, o);
+  SQR_HIP_LAUNCH_CHECK("tail_wgrad_kernel");
+  return 0;
+}

@@ -11,6 +11,7 @@ with ``x.contiguous(memory_format=torch.channels_last)`` (a no-op for the 1-chan
 import torch
 import torch.nn as nn
 
+from sqr import tail
 from sqr.conv import Conv2d
 from sqr.resnet import resnet18
 
@@ -131,17 +132,10 @@ class ResNetSQ(nn.Module):
         self.output_rotation = RotationHead(self.fcn)
 
     def forward(self, x):
+        heads = (self.output_size, self.output_shape, self.output_position, self.output_rotation)
+        if x.is_cuda and tail.supported(self.encoder.fc, heads):
+            # avgpool + encoder.fc + the 4 heads as one fused fp32 op (libsqr sqr_tail_*)
+            return tail.resnet_tail(self.encoder.features(_cl(x)), self.encoder.fc, heads)
         x = self.encoder(_cl(x))  # fp32 features (the encoder's MLP tail runs in fp32)
         with torch.autocast("cuda", enabled=False):
-            x = x.float()
-            heads = (self.output_size, self.output_shape, self.output_position, self.output_rotation)
-            if any(h.dense for h in heads):
-                return tuple(h.forward(x) for h in heads)
-            # the four 256->n heads as ONE 256->12 GEMM (same parameters / state-dict keys):
-            # z = [a | e | t | q] pre-activations, sigmoid on the first 8, L2-normalised quaternion
-            w = torch.cat([h.out_layer[0].weight for h in heads])
-            b = torch.cat([h.out_layer[0].bias for h in heads])
-            z = torch.nn.functional.linear(x, w, b)
-            s = torch.sigmoid(z[:, :8])
-            q = z[:, 8:]
-            return s[:, :3], s[:, 3:5], s[:, 5:8], q / torch.norm(q, 2, -1, keepdim=True)
+            return tuple(h.forward(x.float()) for h in heads)

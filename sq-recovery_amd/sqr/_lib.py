@@ -28,10 +28,23 @@ class SqrPackJob(ctypes.Structure):
     _fields_ = [("w_kcrs", c_void_p), ("desc", SqrConvDesc), ("w_krsc", c_void_p), ("w_crsk", c_void_p)]
 
 
+class SqrTailDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("B", "P", "C0", "F1", "F2", "dtype")] + \
+        [("w0", c_void_p), ("b0", c_void_p), ("w1", c_void_p), ("b1", c_void_p),
+         ("wh", c_void_p * 4), ("bh", c_void_p * 4)]
+
+
+class SqrTailGrads(ctypes.Structure):
+    _fields_ = [("g_out", c_void_p * 4), ("ld", c_int * 4), ("dx", c_void_p), ("dw0", c_void_p),
+                ("db0", c_void_p), ("dw1", c_void_p), ("db1", c_void_p), ("dwh", c_void_p * 4),
+                ("dbh", c_void_p * 4)]
+
+
 # name -> (restype, argtypes); must mirror include/sqr.h exactly
 SIGNATURES = {
     "sqr_version": (c_int, []),
     "sqr_last_error_string": (ctypes.c_char_p, []),
+    "sqr_probe_arm": (c_int, [c_void_p, c_void_p]),
     "sqr_implicit_loss_workspace_bytes": (c_size_t, [c_int, c_int]),
     "sqr_implicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float,
                                           c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -74,6 +87,12 @@ SIGNATURES = {
                              c_void_p]),
     "sqr_stem_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
+    "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p]),
+    "sqr_tail_workspace_bytes": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
+    "sqr_tail_bwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, ctypes.POINTER(SqrTailGrads), c_void_p,
+                             c_size_t, c_void_p]),
 }
 
 

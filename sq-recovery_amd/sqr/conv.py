@@ -16,8 +16,9 @@ from ._lib import SqrConvDesc, SqrPackJob, check, lib, ptr, stream_ptr
 DT_F32, DT_BF16 = 0, 1
 _CL = torch.channels_last
 
-# Optional kernel probe (bench.py): HIP events recorded on the launch stream around every launch
-# of one (phase, conv shape), to time that kernel live inside a training step.
+# Optional kernel probe (bench.py): HIP events recorded by libsqr on the launch stream around the
+# main kernel of every call of one (phase, conv shape) — sqr_probe_arm — to time that kernel live
+# inside a training step (the split-K reduction / im2col launches of the call are outside).
 _probe = {"key": None, "events": []}
 
 
@@ -37,14 +38,15 @@ class _Probe:
 
     def __enter__(self):
         if self.on:
-            self.e0 = torch.cuda.Event(enable_timing=True)
-            self.e0.record()
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for e in self.ev:  # materialise the hipEvent_t (torch creates it lazily on first record)
+                e.record()
+            check(lib().sqr_probe_arm(self.ev[0].cuda_event, self.ev[1].cuda_event), "sqr_probe_arm")
 
     def __exit__(self, *exc):
         if self.on:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            _probe["events"].append((self.e0, e1))
+            lib().sqr_probe_arm(None, None)
+            _probe["events"].append(self.ev)
 
 
 def _desc(N, C, H, W, K, R, S, stride, pad, dtype):

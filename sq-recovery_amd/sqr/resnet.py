@@ -72,16 +72,20 @@ class ResNet18(nn.Module):
             layers.append(BasicBlock(self.inplanes, planes))
         return nn.Sequential(*layers)
 
-    def forward(self, x):
+    def features(self, x):
+        """conv1 .. layer4: the NHWC layer-4 activation (before average pooling)."""
         convs = [m for m in self.modules() if isinstance(m, Conv2d)]
         if x.is_cuda:  # pack every conv weight of this step in one launch
             pack_all(convs, compute_dtype(x))
         count_batches([m for m in self.modules() if isinstance(m, nn.BatchNorm2d)])
         try:
             x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
-            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+            return self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             clear_packed(convs)  # packed weights live on in autograd's saved tensors only
+
+    def forward(self, x):
+        x = self.features(x)
         # the 512-feature MLP tail is tiny: run it in fp32 even under bf16 autocast (one fp32
         # average-pool read of the bf16 activation instead of a cast kernel per Linear)
         x = x.mean((2, 3), dtype=torch.float32) if x.is_cuda else torch.flatten(self.avgpool(x), 1)
