@@ -504,6 +504,25 @@ using namespace sqr;
 using namespace sqr::bn;
 
 // ============================================================================ host side
+// shared with other kernel files (sqr_common.h): BatchNorm coefficients from f32 statistics partials
+// [rows][2][C] (training: batch statistics, running-stat update, save_mean/invstd) or from the
+// running statistics (eval).  coef = [scale C][shift C].
+int sqr::bn_finalize_partials(const float* part, int rows, long long M, int C, const float* gamma, const float* beta,
+                              float* rmean, float* rvar, float momentum, float eps, float* save_mean,
+                              float* save_invstd, float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, part, rows, (int)M, C, gamma, beta, rmean,
+                     rvar, momentum, eps, save_mean, save_invstd, coef);
+  SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel(partials)");
+  return 0;
+}
+
+int sqr::bn_infer_coef(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                       float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(infer_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, gamma, beta, rmean, rvar, eps, coef);
+  SQR_HIP_LAUNCH_CHECK("bn infer_coef_kernel");
+  return 0;
+}
+
 namespace {
 
 struct RedPlan {

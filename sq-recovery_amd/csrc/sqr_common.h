@@ -30,6 +30,13 @@ void probe_end(hipStream_t st);
     }                                                                          \
   } while (0)
 
+// BatchNorm coefficient helpers (sqr_bn.hip): coef = [scale C][shift C]
+int bn_finalize_partials(const float* part, int rows, long long M, int C, const float* gamma, const float* beta,
+                         float* rmean, float* rvar, float momentum, float eps, float* save_mean, float* save_invstd,
+                         float* coef, hipStream_t st);
+int bn_infer_coef(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
+                  float* coef, hipStream_t st);
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery); built on the host

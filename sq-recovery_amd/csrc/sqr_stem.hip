@@ -1,0 +1,701 @@
+// Fused ResNet stem for bf16 training / inference: conv1 (1 -> 64 channels, 7x7, stride 2, pad 3,
+// no bias) + bn1 + ReLU + max-pool(3, 2, 1) of ResNetSQ's resnet18 encoder (torch/models.py:181-184:
+// the grayscale conv1 is the ImageNet kernel summed over RGB), WITHOUT materialising the conv1
+// activation in HBM.
+//
+// At 256 x 256 input the conv1 output is N x 128 x 128 x 64 bf16 (134 MB at N = 64) while its
+// arithmetic is tiny (8.6 GFLOP): a stock pipeline writes it, re-reads it for BN statistics,
+// BN-apply and pooling, keeps it for the backward, and reads it twice more there (BN-backward
+// reduction and apply) plus once for the weight gradient.  Here it lives only in registers/LDS:
+//
+//   forward  S1 stem_stats_kernel : recompute conv1 per 8x32-pixel tile (MFMA, input window in
+//            LDS), per-block BN partials (sum x, sum x^2 of the bf16-rounded values)
+//            finalize (sqr_bn.hip)  : batch mean / invstd, running stats, scale / shift
+//            S2 stem_pool_kernel  : recompute conv1 for a 4x16 pooled tile (+1 halo row / col),
+//            y = bf16(relu(bf16(x) * scale + shift)), 3x3/2 max-pool with torch's first-max tie
+//            rule -> pooled output (bf16) + argmax tap (u8)
+//   backward S3 stem_bwd_kernel   : per 4x32-pixel tile, recompute x, route the pooled gradient to
+//            its argmax pixel (g = dpool * [y > 0]), and accumulate over the whole batch
+//              T1[k][j] = sum_p g[p][k] A[p][j],  T2[k][j] = sum_p x[p][k] A[p][j],  T3[j] = sum_p A[p][j]
+//              sum_p g[p][k],  sum_p g[p][k] x[p][k]
+//            (A = the 7x7 input patch of pixel p, taps j = 8r + s padded to 64) with MFMA
+//            S4 colsum + stem_bwd_finalize_kernel: BN backward in closed form.  The reference's
+//              dx = a*g + k3*x + k2  (a = gamma*invstd, k3 = -a*invstd*dgamma/M, k2 = -a*sum g/M - k3*mean)
+//            is linear in (g, x, 1), so  dW = a*T1 + k3*T2 + k2*T3  and dgamma / dbeta follow from
+//            the two sums: dx itself is never formed.
+//
+// conv1 as MFMA (v_mfma_f32_16x16x32_bf16): rows = 64 output channels (4 blocks of 16), columns =
+// 16 pixels, k = 64 taps (r, s) = (j / 8, j % 8), r, s < 7 real, the padding taps carry zero
+// weight.  A lane's 8 consecutive taps are one input row segment x[2h-3+r][2w-3 .. 2w+4]: 4
+// aligned ds_read_b32 from the LDS window (column offset 4*(w-w0) bytes).  Weights live in
+// registers (8 fragments) for the whole kernel.
+#include <stdint.h>
+#include "sqr_common.h"
+
+namespace sqr {
+namespace stemf {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int KC = 64;           // conv1 output channels
+constexpr int WPITCH = 72;       // LDS window row pitch (elements): 144 B, a multiple of 4 B
+constexpr int GRID_PERSIST = 512;  // persistent grids (fixed: the partial-sum order is part of the result)
+constexpr int PART_BWD = 2 * KC * KC + 3 * KC;  // T1, T2, T3, sum g, sum g*x
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float bf(float v) { return (float)(bf16)v; }  // round to bf16 (RNE)
+__device__ __forceinline__ uint16_t bfbits(float v) { return __builtin_bit_cast(uint16_t, (bf16)v); }
+__device__ __forceinline__ float bits2f(uint32_t b16) { return __uint_as_float(b16 << 16); }
+
+// weight fragments: wf[jb][ks][i] = bf16(w[16 jb + fr][r = 4 ks + fq][s = i]) (0 for r or s == 7)
+__device__ __forceinline__ void load_wfrag(const float* __restrict__ w, int lane, bf16x8 (&wf)[4][2]) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r = 4 * ks + fq;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        wf[jb][ks][i] = (bf16)((r < 7 && i < 7) ? w[(16 * jb + fr) * 49 + r * 7 + i] : 0.f);
+    }
+}
+
+// conv1 of 16 pixels: lane (fr, fq) supplies pixel fr, whose tap (0, 0) sits at byte woff of the
+// window; acc[jb][e] = x[pixel fr][channel 16 jb + 4 fq + e] (fp32)
+__device__ __forceinline__ void conv_block(const char* win, int woff, int lane, const bf16x8 (&wf)[4][2],
+                                           f32x4 (&acc)[4]) {
+  const int fq = lane >> 4;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const char* p = win + woff + (4 * ks + fq) * (WPITCH * 2);
+    const u32x4 u = {*(const uint32_t*)p, *(const uint32_t*)(p + 4), *(const uint32_t*)(p + 8),
+                     *(const uint32_t*)(p + 12)};
+    const bf16x8 a = __builtin_bit_cast(bf16x8, u);
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) acc[jb] = mfma(wf[jb][ks], a, acc[jb]);
+  }
+}
+
+// Input window rows [y0, y0 + WR) x cols [x0, x0 + WC) staged through registers: load() issues
+// the (branch-free, clamped) global loads of a tile early, store() writes them as bf16 into the LDS
+// window (pitch WPITCH) — the persistent loops prefetch tile t+1 while tile t computes.
+template <typename TI, int WR, int WC>
+struct Window {
+  static constexpr int NE = WR * WC, KW = (NE + 255) / 256;
+  float v[KW];
+  __device__ __forceinline__ void load(const TI* __restrict__ img, int H, int W, int y0, int x0) {
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int r = i / WC, c = i - r * WC;
+      const int y = y0 + r, x = x0 + c;
+      const bool ok = i < NE && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const int yc = min(max(y, 0), H - 1), xc = min(max(x, 0), W - 1);
+      const float t = (float)img[(size_t)yc * W + xc];
+      v[k] = ok ? t : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* win) const {
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      const int r = i / WC, c = i - r * WC;
+      if (i < NE) win[r * WPITCH + c] = bfbits(v[k]);
+    }
+  }
+};
+
+// ---------------------------------------------------------------- S1: BN statistics
+// tile = 8 conv rows x 32 conv cols (16 MFMA pixel blocks, 4 per wave); window 22 x 70
+template <typename TI>
+__global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ img, const float* __restrict__ w,
+                                                         int H, int W, int tiles_x, int tiles_img, int ntiles,
+                                                         float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[22 * WPITCH * 2 + 4 * 2 * KC * 4];
+  uint16_t* win = (uint16_t*)smem;
+  float* red = (float*)(smem + 22 * WPITCH * 2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  bf16x8 wf[4][2];
+  load_wfrag(w, lane, wf);
+  float s1[16], s2[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s1[i] = s2[i] = 0.f;
+  Window<TI, 22, 70> pf;
+  auto fetch = [&](int t) {
+    const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    pf.load(img + (size_t)n * H * W, H, W, 16 * ty - 3, 64 * tx - 3);
+  };
+  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // previous tile's window reads are done
+    pf.store(win);
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);  // next tile's loads fly during this one's MFMAs
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int q = (wave * 4 + b) * 16 + fr, py = q >> 5, px = q & 31;
+      f32x4 acc[4];
+      conv_block((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
+      // every tile pixel is a real conv output (Hc % 8 == 0, Wc % 32 == 0 checked on the host)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = bf(acc[jb][e]);
+          s1[jb * 4 + e] += v;
+          s2[jb * 4 + e] = fmaf(v, v, s2[jb * 4 + e]);
+        }
+    }
+  }
+  // reduce over the 16 pixel lanes (fixed xor tree), then over the 4 waves in order
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      s1[i] += __shfl_xor(s1[i], off, 64);
+      s2[i] += __shfl_xor(s2[i], off, 64);
+    }
+  }
+  __syncthreads();
+  if (fr == 0) {
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 16 * jb + 4 * fq + e;
+        red[(wave * 2 + 0) * KC + c] = s1[jb * 4 + e];
+        red[(wave * 2 + 1) * KC + c] = s2[jb * 4 + e];
+      }
+  }
+  __syncthreads();
+  if (tid < 2 * KC) {
+    const int q = tid / KC, c = tid - q * KC;
+    const float v = ((red[(0 * 2 + q) * KC + c] + red[(1 * 2 + q) * KC + c]) + red[(2 * 2 + q) * KC + c]) +
+                    red[(3 * 2 + q) * KC + c];
+    part[((size_t)blockIdx.x * 2 + q) * KC + c] = v;
+  }
+}
+
+// ---------------------------------------------------------------- S2: BN + ReLU + max-pool
+// pooled tile 4 x 16 -> conv region 9 x 33 (rows 2 ph0 - 1 .., cols 2 pw0 - 1 ..) = 297 pixels in
+// 19 blocks; window 24 x 72.  LDS conv tile [297][64] bf16 of the post-ReLU values (-inf outside).
+constexpr int PTH = 4, PTW = 16;
+constexpr int PR = 2 * PTH + 1, PC = 2 * PTW + 1, PPIX = PR * PC, PBLK = (PPIX + 15) / 16;
+constexpr int S2_WR = 2 * (PR - 1) + 8, S2_WC = 2 * (PC - 1) + 8;
+constexpr int S2_WIN = S2_WR * WPITCH * 2;
+constexpr int S2_LDS = S2_WIN + PPIX * KC * 2;
+static_assert(S2_WC <= WPITCH, "window pitch");
+
+template <typename TI>
+__global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ img, const float* __restrict__ w,
+                                                        const float* __restrict__ coef, int H, int W, int Hc, int Wc,
+                                                        int Hp, int Wp, int ptx, int ptiles_img, int ntiles,
+                                                        bf16* __restrict__ y, uint8_t* __restrict__ argmax) {
+  __shared__ __attribute__((aligned(16))) char smem[S2_LDS];
+  uint16_t* win = (uint16_t*)smem;
+  char* tile = smem + S2_WIN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  bf16x8 wf[4][2];
+  load_wfrag(w, lane, wf);
+  float sc[16], sh[16];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sc[jb * 4 + e] = coef[16 * jb + 4 * fq + e];
+      sh[jb * 4 + e] = coef[KC + 16 * jb + 4 * fq + e];
+    }
+  Window<TI, S2_WR, S2_WC> pf;
+  auto fetch = [&](int t) {
+    const int n = t / ptiles_img, rem = t - n * ptiles_img, pty = rem / ptx, ptxx = rem - pty * ptx;
+    pf.load(img + (size_t)n * H * W, H, W, 2 * (2 * pty * PTH - 1) - 3, 2 * (2 * ptxx * PTW - 1) - 3);
+  };
+  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int n = t / ptiles_img, rem = t - n * ptiles_img, pty = rem / ptx, ptxx = rem - pty * ptx;
+    const int ph0 = pty * PTH, pw0 = ptxx * PTW;
+    const int ch0 = 2 * ph0 - 1, cw0 = 2 * pw0 - 1;  // conv origin of the region
+    __syncthreads();
+    pf.store(win);
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
+    for (int b = wave; b < PBLK; b += 4) {
+      const int q = b * 16 + fr;
+      const int qc = q < PPIX ? q : PPIX - 1;
+      const int row = qc / PC, col = qc - row * PC;
+      f32x4 acc[4];
+      conv_block((const char*)win, 2 * row * WPITCH * 2 + 4 * col, lane, wf, acc);
+      const int hc = ch0 + row, wc = cw0 + col;
+      const bool inside = (unsigned)hc < (unsigned)Hc && (unsigned)wc < (unsigned)Wc;
+      if (q < PPIX) {
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) {
+          uint32_t pk[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            uint32_t lo = 0xff80u, hi = 0xff80u;  // bf16 -inf: never selected by the max
+            if (inside) {
+              // the unfused path: bf16 conv output -> relu(x * scale + shift) -> rounded to bf16
+              const int i0 = jb * 4 + 2 * h, i1 = i0 + 1;
+              lo = bfbits(fmaxf(fmaf(bf(acc[jb][2 * h]), sc[i0], sh[i0]), 0.f));
+              hi = bfbits(fmaxf(fmaf(bf(acc[jb][2 * h + 1]), sc[i1], sh[i1]), 0.f));
+            }
+            pk[h] = lo | (hi << 16);
+          }
+          *(u32x2*)(tile + (size_t)q * KC * 2 + (16 * jb + 4 * fq) * 2) = u32x2{pk[0], pk[1]};
+        }
+      }
+    }
+    __syncthreads();
+    // pooling: item = (pooled pixel, 8-channel group)
+#pragma unroll
+    for (int k = 0; k < PTH * PTW * 8 / 256; ++k) {
+      const int it = tid + 256 * k;
+      const int cg = it & 7, pp = it >> 3, i = pp / PTW, j = pp - i * PTW;
+      float best[8];
+      uint32_t bi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        best[e] = -INFINITY;
+        bi[e] = 0;
+      }
+#pragma unroll
+      for (int dh = 0; dh < 3; ++dh)
+#pragma unroll
+        for (int dw = 0; dw < 3; ++dw) {
+          const int q = (2 * i + dh) * PC + 2 * j + dw;
+          const u32x4 u = *(const u32x4*)(tile + (size_t)q * KC * 2 + cg * 16);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = bits2f((u[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+            if (v > best[e]) {  // strict: the first maximum in row-major window order wins (torch)
+              best[e] = v;
+              bi[e] = dh * 3 + dw;
+            }
+          }
+        }
+      const size_t o = (((size_t)n * Hp + ph0 + i) * Wp + pw0 + j) * KC + cg * 8;
+      u32x4 ov;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ov[e] = (uint32_t)bfbits(best[2 * e]) | ((uint32_t)bfbits(best[2 * e + 1]) << 16);
+      *(u32x4*)(y + o) = ov;
+      if (argmax) {
+        u32x2 av;
+        av[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
+        av[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+        *(u32x2*)(argmax + o) = av;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- S3: backward accumulation
+// tile = 4 conv rows x 32 conv cols = 128 pixels (8 blocks, 2 per wave); window 14 x 70 (2016 B,
+// padded to 2 KiB).  LDS images [64 rows][128 px] bf16 (256-B rows, 16-B slot s of row r stored at
+// slot s ^ (r & 15)):  AT[tap j][p] = A[p][j],  GT[k][p] = g,  XT[k][p] = x.  The conv1 weight
+// fragments live in LDS here (8 KiB) to keep the register budget at 2 workgroups per CU.
+constexpr int S3_IMG = 64 * 256;
+constexpr int S3_WF = 8 * 64 * 16;
+constexpr int S3_LDS = 2048 + 3 * S3_IMG + S3_WF;
+
+__device__ __forceinline__ int img_off(int row, int p) {  // byte offset of element p of row
+  return row * 256 + ((((p >> 3) ^ (row & 15))) << 4) + (p & 7) * 2;
+}
+
+// pooled-gradient inputs of one (quad, 8-channel group) item: the 4 pooling windows (K + a, J + b)
+struct PoolIn {
+  u32x2 am[4];
+  u32x4 dp[4], yp[4];
+  uint32_t valid;  // bit a*2+b: window inside the pooled grid
+};
+
+__device__ __forceinline__ void pool_load(PoolIn& pi, const bf16* __restrict__ dpool, const bf16* __restrict__ ypool,
+                                          const uint8_t* __restrict__ argmax, int n, int K, int J, int Hp, int Wp,
+                                          int cg) {
+  pi.valid = 0;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int oh = K + a, ow = J + b;
+      if (oh < Hp && ow < Wp) pi.valid |= 1u << (a * 2 + b);
+      const size_t o = (((size_t)n * Hp + min(oh, Hp - 1)) * Wp + min(ow, Wp - 1)) * KC + cg * 8;
+      pi.am[a * 2 + b] = *(const u32x2*)(argmax + o);
+      pi.dp[a * 2 + b] = *(const u32x4*)(dpool + o);
+      pi.yp[a * 2 + b] = *(const u32x4*)(ypool + o);
+    }
+}
+
+template <typename TI>
+__global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__ img, const float* __restrict__ w,
+                                                          const bf16* __restrict__ dpool,
+                                                          const bf16* __restrict__ ypool,
+                                                          const uint8_t* __restrict__ argmax, int H, int W, int Hp,
+                                                          int Wp, int tiles_x, int tiles_img, int ntiles,
+                                                          float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[S3_LDS];
+  uint16_t* win = (uint16_t*)smem;
+  char* AT = smem + 2048;
+  char* GT = AT + S3_IMG;
+  char* XT = GT + S3_IMG;
+  bf16x8* WF = (bf16x8*)(XT + S3_IMG);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  if (wave == 0) {
+    bf16x8 wf[4][2];
+    load_wfrag(w, lane, wf);
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) WF[(jb * 2 + ks) * 64 + lane] = wf[jb][ks];
+  }
+  f32x4 T1[4], T2[4];
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) T1[jb] = T2[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // g items: thread = (quad = tid >> 3 of 2 x 16 quads, channel group cg = tid & 7)
+  const int cg = tid & 7, quad = tid >> 3, qy = quad >> 4, qx = quad & 15;
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sg[e] = sgx[e] = 0.f;
+  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
+  const int oct = tid & 15;
+  float t3[4] = {0.f, 0.f, 0.f, 0.f};
+
+  // prefetch (registers): the next tile's input window is loaded while this tile's conv runs, its
+  // pooled-gradient inputs while this tile's MFMA accumulation runs
+  Window<TI, 14, 70> pw;
+  PoolIn cur;
+  auto fetch_win = [&](int t) {
+    const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    pw.load(img + (size_t)n * H * W, H, W, 8 * ty - 3, 64 * tx - 3);
+  };
+  auto fetch_pool = [&](int t) {
+    const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
+    pool_load(cur, dpool, ypool, argmax, n, 2 * ty + qy, 16 * tx + qx, Hp, Wp, cg);
+  };
+  if ((int)blockIdx.x < ntiles) {
+    fetch_win(blockIdx.x);
+    fetch_pool(blockIdx.x);
+  }
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const bool more = t + (int)gridDim.x < ntiles;
+    __syncthreads();  // the previous tile's LDS images are consumed
+    pw.store(win);
+    __syncthreads();
+    if (more) fetch_win(t + gridDim.x);
+    // (a) x = conv1 (bf16-rounded) -> XT
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int p = (wave * 2 + b) * 16 + fr, py = p >> 5, px = p & 31;
+      bf16x8 wf[4][2];
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) wf[jb][ks] = WF[(jb * 2 + ks) * 64 + lane];
+      f32x4 acc[4];
+      conv_block((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *(uint16_t*)(XT + img_off(16 * jb + 4 * fq + e, p)) = bfbits(acc[jb][e]);
+    }
+    // (b) A^T from the window, and T3
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = (tid >> 4) + 16 * k, r = j >> 3, s = j & 7;
+      const int p0 = oct * 8, py = p0 >> 5, px0 = p0 & 31;
+      const uint16_t* src = win + (2 * py + r) * WPITCH + 2 * px0 + s;
+      u32x4 v;
+      float ts = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t lo = src[4 * e], hi = src[4 * e + 2];
+        v[e] = lo | (hi << 16);
+        ts += bits2f(lo) + bits2f(hi);
+      }
+      t3[k] += ts;
+      *(u32x4*)(AT + img_off(j, p0)) = v;
+    }
+    __syncthreads();
+    // (c) g = pooled gradient routed to its argmax pixel (only where the pooled output > 0): the
+    // pixels of quad (qy, qx) are covered by the pooling windows (K + a, J + b), a, b in {0, 1}
+    {
+      float g[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[q][e] = 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int wdx = a * 2 + b;
+          const bool ok = (cur.valid >> wdx) & 1u;
+#pragma unroll
+          for (int py = 0; py < 2; ++py)
+#pragma unroll
+            for (int px = 0; px < 2; ++px) {
+              const int dh = py - 2 * a + 1, dw = px - 2 * b + 1;
+              if (dh < 0 || dw < 0) continue;
+              const uint32_t tap = (uint32_t)(dh * 3 + dw);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const uint32_t ae = (cur.am[wdx][e >> 2] >> (8 * (e & 3))) & 0xffu;
+                const float dv = bits2f((cur.dp[wdx][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+                const float yv = bits2f((cur.yp[wdx][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+                if (ok && ae == tap && yv > 0.f) g[py * 2 + px][e] += dv;
+              }
+            }
+        }
+#pragma unroll
+      for (int py = 0; py < 2; ++py) {
+        const int p0 = (2 * qy + py) * 32 + 2 * qx;  // pixels p0, p0 + 1 (px = 0, 1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int c = cg * 8 + e;
+          const uint32_t xx = *(const uint32_t*)(XT + img_off(c, p0));
+          const float g0 = g[py * 2][e], g1 = g[py * 2 + 1][e];
+          sg[e] += g0 + g1;
+          sgx[e] = fmaf(g0, bits2f(xx & 0xffffu), fmaf(g1, bits2f(xx >> 16), sgx[e]));
+          *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)bfbits(g0) | ((uint32_t)bfbits(g1) << 16);
+        }
+      }
+    }
+    if (more) fetch_pool(t + gridDim.x);
+    __syncthreads();
+    // (d) T1 += G^T A, T2 += X^T A over the tile's 128 pixels: wave w owns channels 16w .. 16w+15
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int p = 32 * ks + 8 * fq;
+      const int ch = 16 * wave + fr;
+      const bf16x8 gfr = *(const bf16x8*)(GT + img_off(ch, p));
+      const bf16x8 xfr = *(const bf16x8*)(XT + img_off(ch, p));
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const bf16x8 afr = *(const bf16x8*)(AT + img_off(16 * jb + fr, p));
+        T1[jb] = mfma(gfr, afr, T1[jb]);
+        T2[jb] = mfma(xfr, afr, T2[jb]);
+      }
+    }
+  }
+
+  // ---- per-block partials: [T1 64x64][T2 64x64][T3 64][sum g 64][sum g x 64]
+  float* out = part + (size_t)blockIdx.x * PART_BWD;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = 16 * wave + 4 * fq + e, j = 16 * jb + fr;
+      out[k * KC + j] = T1[jb][e];
+      out[KC * KC + k * KC + j] = T2[jb][e];
+    }
+  __syncthreads();
+  float* red = (float*)AT;  // [256][8] x 2 + [256][4] (spills into GT: both are consumed)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[tid * 8 + e] = sg[e];
+    red[2048 + tid * 8 + e] = sgx[e];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[4096 + tid * 4 + k] = t3[k];
+  __syncthreads();
+  if (tid < 64) {  // channel c = tid: threads cg = c / 8 (quads 0..31), element e = c % 8
+    const int c = tid, g8 = c >> 3, e = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int qd = 0; qd < 32; ++qd) {
+      a += red[(qd * 8 + g8) * 8 + e];
+      b += red[2048 + (qd * 8 + g8) * 8 + e];
+    }
+    out[2 * KC * KC + KC + c] = a;
+    out[2 * KC * KC + 2 * KC + c] = b;
+  } else if (tid < 128) {  // tap j = tid - 64: threads (j % 16) * 16 + o, slot k = j / 16
+    const int j = tid - 64, k = j >> 4, tb = (j & 15) * 16;
+    float a = 0.f;
+    for (int o = 0; o < 16; ++o) a += red[4096 + (tb + o) * 4 + k];
+    out[2 * KC * KC + j] = a;
+  }
+}
+
+// ---------------------------------------------------------------- S4: closed-form BN backward
+// (a) column sums of the per-block partials in float64, rows in a fixed order: block = 64 columns
+// (16 float4) x 16 row lanes, the 16 lane sums added in order through LDS
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int rows, int cols,
+                                                     double* __restrict__ out) {
+  __shared__ double red[16][64];
+  const int q = threadIdx.x & 15, z = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + 4 * q;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c0 < cols) {
+#pragma unroll 8
+    for (int r = z; r < rows; r += 16) {
+      const f32x4 v = *(const f32x4*)(part + (size_t)r * cols + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[z][4 * q + e] = a[e];
+  __syncthreads();
+  if (threadIdx.x < 64 && blockIdx.x * 64 + (int)threadIdx.x < cols) {
+    double s = 0.0;
+    for (int zz = 0; zz < 16; ++zz) s += red[zz][threadIdx.x];
+    out[blockIdx.x * 64 + threadIdx.x] = s;
+  }
+}
+
+// (b) block = output channel k, thread = tap j
+__global__ void __launch_bounds__(64) stem_bwd_finalize_kernel(const double* __restrict__ tot, double M,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd, float* __restrict__ dw,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int k = blockIdx.x, j = threadIdx.x;
+  const double t1 = tot[k * KC + j], t2 = tot[KC * KC + k * KC + j], t3 = tot[2 * KC * KC + j];
+  const double sg = tot[2 * KC * KC + KC + k], sgx = tot[2 * KC * KC + 2 * KC + k];
+  const double is = invstd[k], mu = mean[k];
+  const double dgam = (sgx - mu * sg) * is;  // sum g * xhat
+  const double a = (gamma ? (double)gamma[k] : 1.0) * is;
+  const double k3 = -a * is * dgam / M;
+  const double k2 = -a * sg / M - k3 * mu;
+  const int r = j >> 3, s = j & 7;
+  if (r < 7 && s < 7) dw[k * 49 + r * 7 + s] = (float)(a * t1 + k3 * t2 + k2 * t3);
+  if (j == 0) {
+    if (dgamma) dgamma[k] = (float)dgam;
+    if (dbeta) dbeta[k] = (float)sg;
+  }
+}
+
+}  // namespace stemf
+}  // namespace sqr
+
+using namespace sqr;
+using namespace sqr::stemf;
+
+namespace {
+struct StemGeom {
+  int Hc, Wc, Hp, Wp;
+};
+
+int stem_geom(int N, int H, int W, StemGeom* g) {
+  SQR_CHECK_ARG(N >= 1 && H >= 8 && W >= 8, "stem_fused: bad input %dx%dx%d", N, H, W);
+  g->Hc = (H + 6 - 7) / 2 + 1;
+  g->Wc = (W + 6 - 7) / 2 + 1;
+  g->Hp = (g->Hc + 2 - 3) / 2 + 1;
+  g->Wp = (g->Wc + 2 - 3) / 2 + 1;
+  SQR_CHECK_ARG(g->Hc % 8 == 0 && g->Wc % 32 == 0 && g->Hp % PTH == 0 && g->Wp % PTW == 0,
+                "stem_fused: conv1 output %dx%d must tile by 8x32 (pooled by 4x16)", g->Hc, g->Wc);
+  SQR_CHECK_ARG((long long)N * g->Hp * g->Wp * KC < (1ll << 31), "stem_fused: output too large");
+  return 0;
+}
+
+size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
+extern "C" int sqr_stem_fused_supported(int N, int H, int W) {
+  StemGeom g;
+  return stem_geom(N, H, W, &g) == 0 ? 1 : 0;
+}
+
+extern "C" size_t sqr_stem_fused_workspace_bytes(int N, int H, int W) {
+  StemGeom g;
+  if (stem_geom(N, H, W, &g)) return 0;
+  const size_t fwd = a256((size_t)GRID_PERSIST * 2 * KC * 4) + a256(2 * KC * 4);
+  const size_t bwd = a256((size_t)GRID_PERSIST * PART_BWD * 4) + a256((size_t)PART_BWD * 8);
+  return fwd > bwd ? fwd : bwd;
+}
+
+template <typename TI>
+static void launch_stats(const void* x, int N, int H, int W, const StemGeom& g, const float* w, float* part, int grid,
+                         hipStream_t st) {
+  const int tiles_x = g.Wc / 32, tiles_img = (g.Hc / 8) * tiles_x;
+  hipLaunchKernelGGL(stem_stats_kernel<TI>, dim3(grid), dim3(256), 0, st, (const TI*)x, w, H, W, tiles_x, tiles_img,
+                     N * tiles_img, part);
+}
+
+template <typename TI>
+static void launch_pool(const void* x, int N, int H, int W, const StemGeom& g, const float* w, const float* coef,
+                        void* y, uint8_t* argmax, hipStream_t st) {
+  const int ptx = g.Wp / PTW, ptiles_img = (g.Hp / PTH) * ptx, ntiles = N * ptiles_img;
+  const int grid = ntiles < 768 ? ntiles : 768;  // persistent: 3 workgroups per CU
+  hipLaunchKernelGGL(stem_pool_kernel<TI>, dim3(grid), dim3(256), 0, st, (const TI*)x, w, coef, H, W, g.Hc, g.Wc,
+                     g.Hp, g.Wp, ptx, ptiles_img, ntiles, (bf16*)y, argmax);
+}
+
+extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int N, int H, int W, const float* w, const float* gamma,
+                                  const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                                  int training, void* y, uint8_t* argmax, float* save_mean, float* save_invstd,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  StemGeom g;
+  int rc = stem_geom(N, H, W, &g);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && w && y && workspace, "stem_fused_fwd: null pointer");
+  SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16, "stem_fused_fwd: bad x dtype");
+  SQR_CHECK_ARG(!training || (save_mean && save_invstd), "stem_fused_fwd: training needs save_mean/save_invstd");
+  SQR_CHECK_ARG(training || (running_mean && running_var), "stem_fused_fwd: eval needs running statistics");
+  if (workspace_bytes < sqr_stem_fused_workspace_bytes(N, H, W)) {
+    set_error("stem_fused_fwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* part = (float*)workspace;
+  float* coef = (float*)((char*)workspace + a256((size_t)GRID_PERSIST * 2 * KC * 4));
+  if (training) {
+    const int ntiles = N * (g.Hc / 8) * (g.Wc / 32);
+    const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;
+    if (x_dtype == SQR_DTYPE_BF16) launch_stats<bf16>(x, N, H, W, g, w, part, grid, st);
+    else launch_stats<float>(x, N, H, W, g, w, part, grid, st);
+    SQR_HIP_LAUNCH_CHECK("stem_stats_kernel");
+    rc = bn_finalize_partials(part, grid, (long long)N * g.Hc * g.Wc, KC, gamma, beta, running_mean, running_var,
+                              momentum, eps, save_mean, save_invstd, coef, st);
+  } else {
+    rc = bn_infer_coef(KC, gamma, beta, running_mean, running_var, eps, coef, st);
+  }
+  if (rc) return rc;
+  if (x_dtype == SQR_DTYPE_BF16) launch_pool<bf16>(x, N, H, W, g, w, coef, y, training ? argmax : nullptr, st);
+  else launch_pool<float>(x, N, H, W, g, w, coef, y, training ? argmax : nullptr, st);
+  SQR_HIP_LAUNCH_CHECK("stem_pool_kernel");
+  return 0;
+}
+
+extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int W, const float* w, const float* gamma,
+                                  const float* save_mean, const float* save_invstd, const void* dy, const void* y,
+                                  const uint8_t* argmax, float* dw, float* dgamma, float* dbeta, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  StemGeom g;
+  int rc = stem_geom(N, H, W, &g);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && w && save_mean && save_invstd && dy && y && argmax && dw && workspace,
+                "stem_fused_bwd: null pointer");
+  SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16, "stem_fused_bwd: bad x dtype");
+  if (workspace_bytes < sqr_stem_fused_workspace_bytes(N, H, W)) {
+    set_error("stem_fused_bwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  float* part = (float*)workspace;
+  const int tiles_x = g.Wc / 32, tiles_img = (g.Hc / 4) * tiles_x, ntiles = N * tiles_img;
+  const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;
+  if (x_dtype == SQR_DTYPE_BF16)
+    hipLaunchKernelGGL(stem_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, w, (const bf16*)dy,
+                       (const bf16*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles, part);
+  else
+    hipLaunchKernelGGL(stem_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, w, (const bf16*)dy,
+                       (const bf16*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles, part);
+  SQR_HIP_LAUNCH_CHECK("stem_bwd_kernel");
+  double* tot = (double*)((char*)workspace + a256((size_t)GRID_PERSIST * PART_BWD * 4));
+  hipLaunchKernelGGL(colsum_kernel, dim3((PART_BWD + 63) / 64), dim3(256), 0, st, (const float*)part, grid, PART_BWD,
+                     tot);
+  SQR_HIP_LAUNCH_CHECK("colsum_kernel");
+  hipLaunchKernelGGL(stem_bwd_finalize_kernel, dim3(KC), dim3(64), 0, st, (const double*)tot,
+                     (double)N * g.Hc * g.Wc, gamma, save_mean, save_invstd, dw, dgamma, dbeta);
+  SQR_HIP_LAUNCH_CHECK("stem_bwd_finalize_kernel");
+  return 0;
+}

@@ -89,25 +89,39 @@ __device__ __forceinline__ float wave_dot(const float* __restrict__ w, const flo
   return wave_sum(s);
 }
 
-// y = W x over rows [0, rows): wave w takes rows w, w+4, ... (4 rows in flight per iteration)
+// y = W x over rows [0, rows) (rows % 4 == 0): wave w owns a contiguous quarter of the rows and
+// works through it RB rows at a time with every weight load of the batch in flight together (the
+// weights come from L2 after the first sample's block: this loop is load-latency bound)
+template <int RB>
 __device__ __forceinline__ void rows_dot(const float* __restrict__ W, const float* __restrict__ bias, const float* v,
                                          int rows, int n, int wave, int lane, float* pre_out, float* act_out) {
-  for (int j = wave; j < rows; j += 16) {
-    float s[4];
+  const int per = rows >> 2, rbeg = wave * per, rend = rbeg + per;
+  for (int j = rbeg; j < rend; j += RB) {
+    float s[RB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int r = j + 4 * u;
-      s[u] = r < rows ? wave_dot(W + (size_t)r * n, v, n, lane) : 0.f;
+    for (int u = 0; u < RB; ++u) s[u] = 0.f;
+#pragma unroll 2
+    for (int c = lane * 4; c < n; c += 256) {
+      f32x4 a[RB];
+#pragma unroll
+      for (int u = 0; u < RB; ++u)  // rows past the end re-load the last row (branch-free: loads stay in flight)
+        a[u] = *(const f32x4*)(W + (size_t)min(j + u, rend - 1) * n + c);
+      const f32x4 x = *(const f32x4*)(v + c);
+#pragma unroll
+      for (int u = 0; u < RB; ++u)
+        s[u] = fmaf(a[u][3], x[3], fmaf(a[u][2], x[2], fmaf(a[u][1], x[1], fmaf(a[u][0], x[0], s[u]))));
     }
-    if (lane == 0) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = j + 4 * u;
-        if (r < rows) {
-          const float p = s[u] + bias[r];
-          pre_out[r] = p;
-          act_out[r] = leaky(p);
-        }
+    for (int u = 0; u < RB; ++u) s[u] = wave_sum(s[u]);
+    if (lane < RB) {
+      float mine = s[0];
+#pragma unroll
+      for (int u = 1; u < RB; ++u) mine = lane == u ? s[u] : mine;
+      const int r = j + lane;
+      if (r < rend) {
+        const float p = mine + bias[r];
+        pre_out[r] = p;
+        act_out[r] = leaky(p);
       }
     }
   }
@@ -127,6 +141,7 @@ __global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict_
   {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const T* xn = (const T*)d.x + (size_t)n * d.P * d.C0 + v * 8;
+#pragma unroll 8
     for (int p = ph; p < d.P; p += phases) {
       float t[8];
       IO<T>::load8(xn + (size_t)p * d.C0, t);
@@ -145,9 +160,9 @@ __global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict_
     sv[c] = s;
   }
   __syncthreads();
-  rows_dot(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
+  rows_dot<16>(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
   __syncthreads();
-  rows_dot(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
+  rows_dot<16>(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
   __syncthreads();
   for (int i = wave; i < NOUT; i += 4) {
     const int hd = head_of(i), r = head_row(i);
@@ -293,6 +308,7 @@ __global__ void __launch_bounds__(256) tail_wgrad_kernel(Dev d, const float* __r
   const int ldd = d.F1 + d.F2 + NOUT;
   for (int c = threadIdx.x; c < ncols; c += 256) {
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
     for (int n = 0; n < d.B; ++n) {
       float a = save[(size_t)n * d.ldsave + aoff + c];
       if (sec > 0) a = leaky(a);

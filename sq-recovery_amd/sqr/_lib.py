@@ -87,6 +87,14 @@ SIGNATURES = {
                              c_void_p]),
     "sqr_stem_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_stem_fused_supported": (c_int, [c_int, c_int, c_int]),
+    "sqr_stem_fused_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "sqr_stem_fused_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_size_t, c_void_p]),
+    "sqr_stem_fused_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                   c_void_p]),
     "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p]),

@@ -12,7 +12,7 @@ import warnings
 import torch
 import torch.nn as nn
 
-from .bn import bn_act, count_batches, stem
+from .bn import bn_act, count_batches, fused_stem, fused_stem_ok, stem
 from .conv import Conv2d, clear_packed, compute_dtype, pack_all
 
 
@@ -75,11 +75,18 @@ class ResNet18(nn.Module):
     def features(self, x):
         """conv1 .. layer4: the NHWC layer-4 activation (before average pooling)."""
         convs = [m for m in self.modules() if isinstance(m, Conv2d)]
+        # bf16: conv1 + bn1 + relu + maxpool as one op that never writes the conv1 activation
+        fuse = x.is_cuda and compute_dtype(x) == torch.bfloat16 and fused_stem_ok(x, self.conv1, self.bn1)
+        if fuse:
+            convs = [m for m in convs if m is not self.conv1]
         if x.is_cuda:  # pack every conv weight of this step in one launch
             pack_all(convs, compute_dtype(x))
         count_batches([m for m in self.modules() if isinstance(m, nn.BatchNorm2d)])
         try:
-            x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
+            if fuse:
+                x = fused_stem(x, self.conv1, self.bn1, counted=True)
+            else:
+                x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
             return self.layer4(self.layer3(self.layer2(self.layer1(x))))
         finally:
             clear_packed(convs)  # packed weights live on in autograd's saved tensors only
