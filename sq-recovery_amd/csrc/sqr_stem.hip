@@ -29,6 +29,7 @@
 // weight.  A lane's 8 consecutive taps are one input row segment x[2h-3+r][2w-3 .. 2w+4]: 4
 // aligned ds_read_b32 from the LDS window (column offset 4*(w-w0) bytes).  Weights live in
 // registers (8 fragments) for the whole kernel.
+#include <limits.h>
 #include <stdint.h>
 #include "sqr_common.h"
 
@@ -52,6 +53,17 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 __device__ __forceinline__ float bf(float v) { return (float)(bf16)v; }  // round to bf16 (RNE)
 __device__ __forceinline__ uint16_t bfbits(float v) { return __builtin_bit_cast(uint16_t, (bf16)v); }
 __device__ __forceinline__ float bits2f(uint32_t b16) { return __uint_as_float(b16 << 16); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 pair (RNE; v_cvt_pk_bf16_f32), lo in bits 0..15
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+}
+// ReLU of a packed bf16 pair as signed 16-bit max with 0 (negative values and -0 -> +0)
+__device__ __forceinline__ uint32_t pk_relu(uint32_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), s16x2{0, 0}));
+}
 
 // weight fragments: wf[jb][ks][i] = bf16(w[16 jb + fr][r = 4 ks + fq][s = i]) (0 for r or s == 7)
 __device__ __forceinline__ void load_wfrag(const float* __restrict__ w, int lane, bf16x8 (&wf)[4][2]) {
@@ -187,12 +199,14 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
 
 // ---------------------------------------------------------------- S2: BN + ReLU + max-pool
 // pooled tile 4 x 16 -> conv region 9 x 33 (rows 2 ph0 - 1 .., cols 2 pw0 - 1 ..) = 297 pixels in
-// 19 blocks; window 24 x 72.  LDS conv tile [297][64] bf16 of the post-ReLU values (-inf outside).
+// 19 blocks; window 24 x 72.  LDS conv tile [297][64] bf16 (pixel pitch 144 B) of the post-ReLU
+// values (-inf outside the image).
 constexpr int PTH = 4, PTW = 16;
 constexpr int PR = 2 * PTH + 1, PC = 2 * PTW + 1, PPIX = PR * PC, PBLK = (PPIX + 15) / 16;
 constexpr int S2_WR = 2 * (PR - 1) + 8, S2_WC = 2 * (PC - 1) + 8;
 constexpr int S2_WIN = S2_WR * WPITCH * 2;
-constexpr int S2_LDS = S2_WIN + PPIX * KC * 2;
+constexpr int TPITCH = KC * 2 + 16;  // conv tile pixel pitch (bytes): 144 = 36 dwords spreads a wave's pixels over the banks
+constexpr int S2_LDS = S2_WIN + PPIX * TPITCH;
 static_assert(S2_WC <= WPITCH, "window pitch");
 
 template <typename TI>
@@ -242,16 +256,14 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
           uint32_t pk[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            uint32_t lo = 0xff80u, hi = 0xff80u;  // bf16 -inf: never selected by the max
-            if (inside) {
-              // the unfused path: bf16 conv output -> relu(x * scale + shift) -> rounded to bf16
-              const int i0 = jb * 4 + 2 * h, i1 = i0 + 1;
-              lo = bfbits(fmaxf(fmaf(bf(acc[jb][2 * h]), sc[i0], sh[i0]), 0.f));
-              hi = bfbits(fmaxf(fmaf(bf(acc[jb][2 * h + 1]), sc[i1], sh[i1]), 0.f));
-            }
-            pk[h] = lo | (hi << 16);
+            // the unfused path: bf16 conv output -> relu(x * scale + shift) -> rounded to bf16
+            const int i0 = jb * 4 + 2 * h, i1 = i0 + 1;
+            const uint32_t xb = pk_bf16(acc[jb][2 * h], acc[jb][2 * h + 1]);
+            const float t0 = fmaf(__uint_as_float(xb << 16), sc[i0], sh[i0]);
+            const float t1 = fmaf(__uint_as_float(xb & 0xffff0000u), sc[i1], sh[i1]);
+            pk[h] = inside ? pk_relu(pk_bf16(t0, t1)) : 0xff80ff80u;  // bf16 -inf outside the image
           }
-          *(u32x2*)(tile + (size_t)q * KC * 2 + (16 * jb + 4 * fq) * 2) = u32x2{pk[0], pk[1]};
+          *(u32x2*)(tile + (size_t)q * TPITCH + (16 * jb + 4 * fq) * 2) = u32x2{pk[0], pk[1]};
         }
       }
     }
@@ -261,37 +273,35 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
     for (int k = 0; k < PTH * PTW * 8 / 256; ++k) {
       const int it = tid + 256 * k;
       const int cg = it & 7, pp = it >> 3, i = pp / PTW, j = pp - i * PTW;
-      float best[8];
-      uint32_t bi[8];
+      // max over the window of the key (value bits << 16 | 15 - tap) as signed int: the values are
+      // bf16 relu outputs (>= +0, integer-ordered) or -inf (negative); on equal values the larger
+      // key is the smaller tap, i.e. torch's first maximum in row-major window order
+      int best[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        best[e] = -INFINITY;
-        bi[e] = 0;
-      }
+      for (int e = 0; e < 8; ++e) best[e] = INT_MIN;
 #pragma unroll
       for (int dh = 0; dh < 3; ++dh)
 #pragma unroll
         for (int dw = 0; dw < 3; ++dw) {
           const int q = (2 * i + dh) * PC + 2 * j + dw;
-          const u32x4 u = *(const u32x4*)(tile + (size_t)q * KC * 2 + cg * 16);
+          const u32x4 u = *(const u32x4*)(tile + (size_t)q * TPITCH + cg * 16);
+          const uint32_t low = 15u - (uint32_t)(dh * 3 + dw);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float v = bits2f((u[e >> 1] >> (16 * (e & 1))) & 0xffffu);
-            if (v > best[e]) {  // strict: the first maximum in row-major window order wins (torch)
-              best[e] = v;
-              bi[e] = dh * 3 + dw;
-            }
+          for (int h = 0; h < 4; ++h) {
+            best[2 * h] = max(best[2 * h], (int)((u[h] << 16) | low));
+            best[2 * h + 1] = max(best[2 * h + 1], (int)((u[h] & 0xffff0000u) | low));
           }
         }
       const size_t o = (((size_t)n * Hp + ph0 + i) * Wp + pw0 + j) * KC + cg * 8;
       u32x4 ov;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) ov[e] = (uint32_t)bfbits(best[2 * e]) | ((uint32_t)bfbits(best[2 * e + 1]) << 16);
+      for (int h = 0; h < 4; ++h)
+        ov[h] = ((uint32_t)best[2 * h] >> 16) | ((uint32_t)best[2 * h + 1] & 0xffff0000u);
       *(u32x4*)(y + o) = ov;
       if (argmax) {
-        u32x2 av;
-        av[0] = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
-        av[1] = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
+        u32x2 av = {0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) av[e >> 2] |= (15u - ((uint32_t)best[e] & 15u)) << (8 * (e & 3));
         *(u32x2*)(argmax + o) = av;
       }
     }
@@ -300,15 +310,18 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
 
 // ---------------------------------------------------------------- S3: backward accumulation
 // tile = 4 conv rows x 32 conv cols = 128 pixels (8 blocks, 2 per wave); window 14 x 70 (2016 B,
-// padded to 2 KiB).  LDS images [64 rows][128 px] bf16 (256-B rows, 16-B slot s of row r stored at
-// slot s ^ (r & 15)):  AT[tap j][p] = A[p][j],  GT[k][p] = g,  XT[k][p] = x.  The conv1 weight
-// fragments live in LDS here (8 KiB) to keep the register budget at 2 workgroups per CU.
+// padded to 2 KiB).  LDS images [64 rows][128 px] bf16 (256-B rows, XOR-swizzled 16-B slots, img_off):
+// AT[tap j][p] = A[p][j],  GT[k][p] = g,  XT[k][p] = x.  The conv1 weight fragments are kept in LDS
+// (8 KiB, read per conv block) so that two workgroups fit a CU's register file.
 constexpr int S3_IMG = 64 * 256;
 constexpr int S3_WF = 8 * 64 * 16;
 constexpr int S3_LDS = 2048 + 3 * S3_IMG + S3_WF;
 
-__device__ __forceinline__ int img_off(int row, int p) {  // byte offset of element p of row
-  return row * 256 + ((((p >> 3) ^ (row & 15))) << 4) + (p & 7) * 2;
+// byte offset of element p of row: 16-B slot (p / 8) ^ key(row), key = (row & 15) ^ ((row >> 3) & 7) is
+// injective both on 16 consecutive rows (the MFMA fragment reads) and on rows 8 apart (the g / x
+// accesses of one pixel pair across a thread's 8 channels)
+__device__ __forceinline__ int img_off(int row, int p) {
+  return row * 256 + ((((p >> 3) ^ ((row & 15) ^ ((row >> 3) & 7)))) << 4) + (p & 7) * 2;
 }
 
 // pooled-gradient inputs of one (quad, 8-channel group) item: the 4 pooling windows (K + a, J + b)
@@ -357,42 +370,51 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) WF[(jb * 2 + ks) * 64 + lane] = wf[jb][ks];
   }
-  f32x4 T1[4], T2[4];
+  f32x4 T1[4], T2[4], T3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb) T1[jb] = T2[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.f;
   // g items: thread = (quad = tid >> 3 of 2 x 16 quads, channel group cg = tid & 7)
   const int cg = tid & 7, quad = tid >> 3, qy = quad >> 4, qx = quad & 15;
   float sg[8], sgx[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) sg[e] = sgx[e] = 0.f;
-  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
-  const int oct = tid & 15;
-  float t3[4] = {0.f, 0.f, 0.f, 0.f};
+  const int oct = tid & 15;  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
 
-  // prefetch (registers): the next tile's input window is loaded while this tile's conv runs, its
-  // pooled-gradient inputs while this tile's MFMA accumulation runs
+  // register prefetch of the next tile's input window and pooled-gradient inputs
   Window<TI, 14, 70> pw;
-  PoolIn cur;
-  auto fetch_win = [&](int t) {
+  PoolIn pin;
+  auto fetch = [&](int t) {
     const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
     pw.load(img + (size_t)n * H * W, H, W, 8 * ty - 3, 64 * tx - 3);
+    pool_load(pin, dpool, ypool, argmax, n, 2 * ty + qy, 16 * tx + qx, Hp, Wp, cg);
   };
-  auto fetch_pool = [&](int t) {
-    const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
-    pool_load(cur, dpool, ypool, argmax, n, 2 * ty + qy, 16 * tx + qx, Hp, Wp, cg);
-  };
-  if ((int)blockIdx.x < ntiles) {
-    fetch_win(blockIdx.x);
-    fetch_pool(blockIdx.x);
-  }
+  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const bool more = t + (int)gridDim.x < ntiles;
     __syncthreads();  // the previous tile's LDS images are consumed
     pw.store(win);
-    __syncthreads();
-    if (more) fetch_win(t + gridDim.x);
-    // (a) x = conv1 (bf16-rounded) -> XT
+    // the pooled inputs of this tile, reduced to what the routing needs: per window and channel the
+    // argmax tap and the gradient masked by (window valid, pooled output > 0)
+    uint32_t amw[4][2], dvp[4][4];  // dvp: bf16 pairs of the masked gradient
 #pragma unroll
+    for (int wd = 0; wd < 4; ++wd) {
+      const bool ok = (pin.valid >> wd) & 1u;
+      amw[wd][0] = pin.am[wd][0];
+      amw[wd][1] = pin.am[wd][1];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        // pooled values are relu outputs (>= 0): y > 0 <=> its bf16 bits are non-zero
+        const uint32_t y2 = pin.yp[wd][h], d2 = pin.dp[wd][h];
+        const uint32_t mlo = (ok && (y2 & 0xffffu)) ? 0xffffu : 0u, mhi = (ok && (y2 >> 16)) ? 0xffff0000u : 0u;
+        dvp[wd][h] = d2 & (mlo | mhi);
+      }
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
+    // (a) x = conv1 (bf16-rounded) -> XT
+#pragma unroll 1
     for (int b = 0; b < 2; ++b) {
       const int p = (wave * 2 + b) * 16 + fr, py = p >> 5, px = p & 31;
       bf16x8 wf[4][2];
@@ -407,71 +429,55 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
 #pragma unroll
         for (int e = 0; e < 4; ++e) *(uint16_t*)(XT + img_off(16 * jb + 4 * fq + e, p)) = bfbits(acc[jb][e]);
     }
-    // (b) A^T from the window, and T3
+    // (b) A^T from the window
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int j = (tid >> 4) + 16 * k, r = j >> 3, s = j & 7;
       const int p0 = oct * 8, py = p0 >> 5, px0 = p0 & 31;
       const uint16_t* src = win + (2 * py + r) * WPITCH + 2 * px0 + s;
       u32x4 v;
-      float ts = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t lo = src[4 * e], hi = src[4 * e + 2];
-        v[e] = lo | (hi << 16);
-        ts += bits2f(lo) + bits2f(hi);
-      }
-      t3[k] += ts;
+      for (int e = 0; e < 4; ++e) v[e] = (uint32_t)src[4 * e] | ((uint32_t)src[4 * e + 2] << 16);
       *(u32x4*)(AT + img_off(j, p0)) = v;
     }
     __syncthreads();
-    // (c) g = pooled gradient routed to its argmax pixel (only where the pooled output > 0): the
-    // pixels of quad (qy, qx) are covered by the pooling windows (K + a, J + b), a, b in {0, 1}
-    {
-      float g[4][8];
+    // (c) g = pooled gradient routed to its argmax pixel: pixel (py, px) of quad (qy, qx) is tap
+    // (py - 2a + 1, px - 2b + 1) of pooling window (K + a, J + b), a, b in {0, 1}
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+    for (int py = 0; py < 2; ++py) {
+      float g[2][8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) g[q][e] = 0.f;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int wdx = a * 2 + b;
-          const bool ok = (cur.valid >> wdx) & 1u;
-#pragma unroll
-          for (int py = 0; py < 2; ++py)
-#pragma unroll
-            for (int px = 0; px < 2; ++px) {
-              const int dh = py - 2 * a + 1, dw = px - 2 * b + 1;
-              if (dh < 0 || dw < 0) continue;
-              const uint32_t tap = (uint32_t)(dh * 3 + dw);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const uint32_t ae = (cur.am[wdx][e >> 2] >> (8 * (e & 3))) & 0xffu;
-                const float dv = bits2f((cur.dp[wdx][e >> 1] >> (16 * (e & 1))) & 0xffffu);
-                const float yv = bits2f((cur.yp[wdx][e >> 1] >> (16 * (e & 1))) & 0xffffu);
-                if (ok && ae == tap && yv > 0.f) g[py * 2 + px][e] += dv;
-              }
-            }
-        }
-#pragma unroll
-      for (int py = 0; py < 2; ++py) {
-        const int p0 = (2 * qy + py) * 32 + 2 * qx;  // pixels p0, p0 + 1 (px = 0, 1)
+      for (int px = 0; px < 2; ++px)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int c = cg * 8 + e;
-          const uint32_t xx = *(const uint32_t*)(XT + img_off(c, p0));
-          const float g0 = g[py * 2][e], g1 = g[py * 2 + 1][e];
-          sg[e] += g0 + g1;
-          sgx[e] = fmaf(g0, bits2f(xx & 0xffffu), fmaf(g1, bits2f(xx >> 16), sgx[e]));
-          *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)bfbits(g0) | ((uint32_t)bfbits(g1) << 16);
+          float acc = 0.f;
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              const int dh = py - 2 * a + 1, dw = px - 2 * b + 1;
+              if (dh < 0 || dw < 0) continue;
+              const uint32_t ae = (amw[a * 2 + b][e >> 2] >> (8 * (e & 3))) & 0xffu;
+              const uint32_t d2 = dvp[a * 2 + b][e >> 1];
+              const float dv = (e & 1) ? __uint_as_float(d2 & 0xffff0000u) : __uint_as_float(d2 << 16);
+              acc += ae == (uint32_t)(dh * 3 + dw) ? dv : 0.f;
+            }
+          g[px][e] = acc;
         }
+      const int p0 = (2 * qy + py) * 32 + 2 * qx;  // pixels p0, p0 + 1 (px = 0, 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cg * 8 + e;
+        const uint32_t xx = *(const uint32_t*)(XT + img_off(c, p0));
+        const float g0 = g[0][e], g1 = g[1][e];
+        sg[e] += g0 + g1;
+        sgx[e] = fmaf(g0, __uint_as_float(xx << 16), fmaf(g1, __uint_as_float(xx & 0xffff0000u), sgx[e]));
+        *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)bfbits(g0) | ((uint32_t)bfbits(g1) << 16);
       }
     }
-    if (more) fetch_pool(t + gridDim.x);
     __syncthreads();
-    // (d) T1 += G^T A, T2 += X^T A over the tile's 128 pixels: wave w owns channels 16w .. 16w+15
+    // (d) T1 += G^T A, T2 += X^T A over the tile's 128 pixels: wave w owns channels 16w .. 16w+15;
+    // T3 (column sums of A) for taps 16w .. 16w+15 with a ones operand
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int p = 32 * ks + 8 * fq;
@@ -484,6 +490,8 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
         T1[jb] = mfma(gfr, afr, T1[jb]);
         T2[jb] = mfma(xfr, afr, T2[jb]);
       }
+      // (MFMA ignores EXEC: no lane-divergent branch around it)
+      T3 = mfma(ones, *(const bf16x8*)(AT + img_off(ch, p)), T3);
     }
   }
 
@@ -497,15 +505,14 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
       out[k * KC + j] = T1[jb][e];
       out[KC * KC + k * KC + j] = T2[jb][e];
     }
+  if (fq == 0) out[2 * KC * KC + 16 * wave + fr] = T3[0];  // every row of the ones-product is the column sum
   __syncthreads();
-  float* red = (float*)AT;  // [256][8] x 2 + [256][4] (spills into GT: both are consumed)
+  float* red = (float*)AT;  // [256][8] x 2 (spills into GT: both are consumed)
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     red[tid * 8 + e] = sg[e];
     red[2048 + tid * 8 + e] = sgx[e];
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) red[4096 + tid * 4 + k] = t3[k];
   __syncthreads();
   if (tid < 64) {  // channel c = tid: threads cg = c / 8 (quads 0..31), element e = c % 8
     const int c = tid, g8 = c >> 3, e = c & 7;
@@ -516,11 +523,6 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
     }
     out[2 * KC * KC + KC + c] = a;
     out[2 * KC * KC + 2 * KC + c] = b;
-  } else if (tid < 128) {  // tap j = tid - 64: threads (j % 16) * 16 + o, slot k = j / 16
-    const int j = tid - 64, k = j >> 4, tb = (j & 15) * 16;
-    float a = 0.f;
-    for (int o = 0; o < 16; ++o) a += red[4096 + (tb + o) * 4 + k];
-    out[2 * KC * KC + j] = a;
   }
 }
 

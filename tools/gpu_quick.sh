@@ -21,5 +21,6 @@ if [ -n "$PROF" ]; then
   python tools/trace_summary.py "$OUT/prof" 900 > "$OUT/trace_tail.txt"
   find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
   rm -rf "$OUT/prof"
-  python tools/kstats.py "$OUT/kernel_stats.csv" 33 | head -40
+  python tools/kstats.py "$OUT/kernel_stats.csv" 33 > "$OUT/kstats.txt"
+  head -40 "$OUT/kstats.txt"
 fi
