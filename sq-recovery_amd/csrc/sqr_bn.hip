@@ -57,8 +57,8 @@ template <> struct V8<float> {
 __device__ __forceinline__ void load8f(const float* p, float* v) { V8<float>::load(p, v); }
 
 // block geometry for the reductions: V = C/8 channel vectors per pixel, rows = 256 / V
-// partial layout: part[blk][2][C] doubles (sum a, sum b).  4 pixels per iteration per thread so
-// that 4 independent 16-B loads are in flight (the loop is otherwise latency-bound).
+// partial layout: part[blk][2][C] doubles (sum a, sum b).  8 pixels per iteration per thread so
+// that 8 (16 in the backward) independent 16-B loads are in flight (the loop is latency-bound).
 template <typename T, int MODE>
 // MODE 0: a = x, b = x^2                                  (forward statistics)
 // MODE 1: g = dy*[relu bit]; a = g, b = g*(x - mean)     (backward; mask = NULL: no ReLU)
@@ -75,30 +75,32 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
   float mu[8];
   if (MODE == 1) load8f(mean + v * 8, mu);
   const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
-  constexpr int U = 4;
+  constexpr int U = 8;
   for (int pb = p0 + row; pb < p1; pb += U * rows) {
     float xv[U][8], g[U][8];
+    // branch-free loads (rows past the chunk re-read its last pixel and are masked out below):
+    // all U loads stay in flight together
+    uint32_t mbits[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = pb + u * rows;
-      if (p < p1) {
-        const size_t off = (size_t)p * C + v * 8;
-        V8<T>::load(x + off, xv[u]);
-        if (MODE == 1) {
-          V8<T>::load(dy + off, g[u]);
-          if (mask) {
-            const uint32_t mb = mask[off >> 3];
+      const int p = min(pb + u * rows, p1 - 1);
+      const size_t off = (size_t)p * C + v * 8;
+      V8<T>::load(x + off, xv[u]);
+      if (MODE == 1) {
+        V8<T>::load(dy + off, g[u]);
+        mbits[u] = mask ? (uint32_t)mask[off >> 3] : 0xffu;
+      }
+    }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) g[u][i] = (mb >> i) & 1 ? g[u][i] : 0.f;
-          }
-        }
+    for (int u = 0; u < U; ++u) {
+      const bool in = pb + u * rows < p1;
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[u][i] = in ? xv[u][i] : 0.f;
       } else {
+        const uint32_t mb = in ? mbits[u] : 0u;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xv[u][i] = g[u][i] = 0.f;
-        if (MODE == 1) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) xv[u][i] = mu[i];
-        }
+        for (int i = 0; i < 8; ++i) g[u][i] = (mb >> i) & 1 ? g[u][i] : 0.f;
       }
     }
 #pragma unroll
@@ -122,21 +124,13 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
     dst[8 + i] = sb[i];
   }
   __syncthreads();
-  if (row == 0) {
-    for (int r = 1; r < rows; ++r) {
-      const double* src = red + ((size_t)r * V + v) * 16;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        sa[i] += src[i];
-        sb[i] += src[8 + i];
-      }
-    }
-    double* out = part + (size_t)blockIdx.x * 2 * C;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      out[v * 8 + i] = sa[i];
-      out[C + v * 8 + i] = sb[i];
-    }
+  // fixed-order sum over the rows, one thread per (channel vector, statistic, lane element)
+  double* out = part + (size_t)blockIdx.x * 2 * C;
+  for (int t = tid; t < V * 16; t += 256) {
+    const int vv = t >> 4, i = t & 15;
+    double acc = 0.0;
+    for (int r = 0; r < rows; ++r) acc += red[((size_t)r * V + vv) * 16 + i];
+    out[(i >> 3) * C + vv * 8 + (i & 7)] = acc;
   }
 }
 
