@@ -2,8 +2,9 @@
 
 One step = torch/train.py's step (train.py:86-103) on a synthetic batch: ResNetSQ forward (HIP
 implicit-GEMM convs, bf16 autocast), ImplicitLoss(32, tau=1.5, s=260) on the input depth images
-(fused HIP loss + analytic grad, fp32), backward, Adam(lr=1e-4) step — plus, for N>1, DDP's
-bucketed RCCL all-reduce of the gradients overlapped with backward.  Per-GPU batch 64
+(fused HIP loss + analytic grad, fp32), backward, Adam(lr=1e-4) step (sqr.optim.Adam: the same
+update as torch.optim.Adam in libsqr's fused kernel) — plus, for N>1, DDP's bucketed RCCL
+all-reduce of the gradients overlapped with backward.  Per-GPU batch 64
 (BASELINE config 2; config 3 = 8 GPUs x 64).
 
 Synthetic data: SQ parameters drawn from the reference's generator distribution
@@ -85,6 +86,7 @@ def main():
     import models
     from sqr import conv as sconv
     from sqr import losses
+    from sqr import optim as sqr_optim
 
     B, R, H = args.batch, args.render, 256
     rng = np.random.default_rng(1234 + rank)
@@ -96,7 +98,8 @@ def main():
     state0 = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
     model = dist.wrap(net, dev)  # DDP (RCCL all-reduce overlapped with backward) when world > 1
     use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4, weight_decay=0, fused=True, capturable=use_graph)
+    # torch.optim.Adam's semantics on libsqr's fused step (also writes the bf16 packed conv weights)
+    opt = sqr_optim.Adam(net.parameters(), lr=1e-4, weight_decay=0).attach(net)
     crit = classes.ImplicitLoss(R, dev, 1.5, 260)
 
     def body():

@@ -26,6 +26,7 @@
  *                              BasicBlock (ResNetSQ encoder, torch/models.py:181), training and eval.
  *   sqr_stem_fwd / _bwd        resnet18 stem bn1 -> relu -> maxpool(3,2,1) (torch/models.py:181).
  *   sqr_stem_fused_fwd / _bwd  the same stem + conv1 (torch/models.py:181-184) in one pass, bf16.
+ *   sqr_adam_step              torch.optim.Adam step of torch/train.py:50-54 (+ conv weight packing).
  *   sqr_tail_fwd / _bwd        ResNetSQ avgpool + encoder.fc + output heads (torch/models.py:7-99,186-204).
  */
 #ifndef SQR_H
@@ -214,6 +215,27 @@ int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int W, const fl
                        const float* save_mean, const float* save_invstd, const void* dy, const void* y,
                        const uint8_t* argmax, float* dw, float* dgamma, float* dbeta, void* workspace,
                        size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- optimizer */
+
+/* One torch.optim.Adam step (weight_decay 0, no amsgrad / maximize; torch/train.py:50-54) over up to
+ * 80 fp32 parameters, fused with the bf16 packing of conv weights: when w_krsc is set (desc: the
+ * conv geometry, dtype BF16) the updated weight is also written as sqr_conv2d_pack_weight's w_krsc
+ * (and w_crsk when set; K, C multiples of 64).  step: the parameter's device step counter (float),
+ * read as t = step + 1 for the bias corrections and incremented.  params is a host array. */
+typedef struct sqr_adam_param {
+  float* p;
+  const float* g;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;
+  long long n;
+  sqr_conv_desc desc;
+  void* w_krsc; /* nullable */
+  void* w_crsk; /* nullable */
+} sqr_adam_param;
+int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2, double eps,
+                  void* stream);
 
 /* ---------------------------------------------------------------- ResNetSQ tail (fused) */
 

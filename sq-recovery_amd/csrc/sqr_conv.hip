@@ -561,7 +561,19 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   if (qidx < K * nq) {
     const int k = qidx / nq, col0 = (qidx - k * nq) * 4;
     const float* src = slab + (size_t)k * Ng + col0;
-    for (int z = zl; z < splits; z += 16) acc += *(const f32x4*)(src + z * stride);
+    int z = zl;
+    // 4 independent loads in flight per step (the split count is a runtime value)
+    for (; z + 48 < splits; z += 64) {
+      const f32x4 a0 = *(const f32x4*)(src + (size_t)z * stride);
+      const f32x4 a1 = *(const f32x4*)(src + (size_t)(z + 16) * stride);
+      const f32x4 a2 = *(const f32x4*)(src + (size_t)(z + 32) * stride);
+      const f32x4 a3 = *(const f32x4*)(src + (size_t)(z + 48) * stride);
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; z < splits; z += 16) acc += *(const f32x4*)(src + (size_t)z * stride);
   }
   part[zl][ql] = acc;
   __syncthreads();

@@ -1,0 +1,258 @@
+// Adam step fused with the bf16 weight packing of the conv kernels.
+//
+// torch.optim.Adam (the optimizer of torch/train.py:50-54, lr 1e-4) updates every fp32 parameter;
+// the HIP convs then need each conv weight in two bf16 layouts (sqr_conv2d_pack_weight): [K][R][S][C]
+// for forward / weight-gradient and the stride-parity classes [C][Rc][Sc][K] for backward-data.
+// Done separately that is a multi-tensor Adam pass plus a packing pass per step that re-reads the
+// fresh fp32 weights.  Here:
+//   adam_kernel : Adam on every parameter (weight_decay 0, no amsgrad, no maximize) — for a conv
+//                 weight one workgroup per output channel k updates the row w[k][:][:][:] and writes
+//                 its [R][S][C] bf16 image straight from registers/LDS (the w_krsc row);
+//   crsk_kernel : w_crsk from w_krsc by 64 x 64 (k, c) tile transposes per tap through LDS, and the
+//                 per-parameter step counters += 1.
+// Update arithmetic follows torch.optim.Adam's single-tensor path in fp32 with fp64 bias
+// corrections: m = lerp(m, g, 1 - b1); v = b2 v + (1 - b2) g^2;
+// p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps),  t = step + 1.
+#include <stdint.h>
+#include "sqr_common.h"
+
+namespace sqr {
+namespace optim {
+
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int MAXJ = 40;      // jobs per launch (kernel-argument table)
+constexpr int CHUNK = 2048;   // elements per workgroup of a plain (non-conv) parameter
+
+struct Job {
+  float *p, *m, *v;
+  const float* g;
+  const float* step;
+  bf16* krsc;       // conv weight: packed [K][R][S][C] (or [K][Kp] for C < 8), else null
+  int n;            // elements
+  int K, C, RS, Kp; // conv geometry (krsc != null)
+};
+struct Jobs {
+  Job j[MAXJ];
+  int start[MAXJ + 1];  // first workgroup of each job
+  int njobs;
+  double lr, b1, b2;   // as torch's Python scalars
+  float fb2, eps;
+  float omb1, omb2;    // 1 - b1, 1 - b2 (computed in double, as torch does)
+};
+
+// torch's multi-tensor Adam, operation by operation (explicitly rounded: no fma contraction):
+// lerp_(g, 1 - b1); mul_(b2); addcmul_(g, g, 1 - b2); sqrt / bc2_sqrt + eps; addcdiv_(m, denom, -step_size)
+__device__ __forceinline__ void adam_update(float& p, float& m, float& v, float g, float omb1, float b2, float omb2,
+                                            float step_size, float bc2s, float eps) {
+  m = __fadd_rn(m, __fmul_rn(omb1, __fsub_rn(g, m)));  // lerp with weight 1 - b1 < 0.5
+  v = __fadd_rn(__fmul_rn(v, b2), __fmul_rn(__fmul_rn(omb2, g), g));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2s), eps);
+  p = __fadd_rn(p, __fmul_rn(-step_size, __fdiv_rn(m, denom)));
+}
+
+__global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
+  extern __shared__ float lds[];
+  const int b = blockIdx.x;
+  int ji = 0;
+  while (ji + 1 < J.njobs && b >= J.start[ji + 1]) ++ji;
+  const Job& jb = J.j[ji];
+  const int local = b - J.start[ji];
+  const double t = (double)(*jb.step) + 1.0;
+  const double bc1 = 1.0 - pow(J.b1, t), bc2 = 1.0 - pow(J.b2, t);
+  const float step_size = (float)(J.lr / bc1), bc2s = (float)sqrt(bc2);
+  if (!jb.krsc) {
+    const int i0 = local * CHUNK;
+    const int i1 = min(i0 + CHUNK, jb.n);
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) {
+      float p = jb.p[i], m = jb.m[i], v = jb.v[i];
+      adam_update(p, m, v, jb.g[i], J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+      jb.p[i] = p;
+      jb.m[i] = m;
+      jb.v[i] = v;
+    }
+    return;
+  }
+  // conv weight: row k = local, CRS = C * RS contiguous elements w[k][c][tap]
+  const int k = local, CRS = jb.C * jb.RS;
+  const size_t base = (size_t)k * CRS;
+  for (int i = threadIdx.x; i < CRS; i += 256) {
+    float p = jb.p[base + i], m = jb.m[base + i], v = jb.v[base + i];
+    adam_update(p, m, v, jb.g[base + i], J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+    jb.p[base + i] = p;
+    jb.m[base + i] = m;
+    jb.v[base + i] = v;
+    lds[i] = p;
+  }
+  __syncthreads();
+  // krsc[k][tap][c] (row length Kp >= RS*C; the im2col padding is zero)
+  bf16* __restrict__ dst = jb.krsc + (size_t)k * jb.Kp;
+  for (int i = threadIdx.x; i < jb.Kp; i += 256) {
+    float val = 0.f;
+    if (i < CRS) {
+      const int tap = i / jb.C, c = i - tap * jb.C;
+      val = lds[c * jb.RS + tap];
+    }
+    dst[i] = (bf16)val;
+  }
+}
+
+struct CJob {
+  const bf16* krsc;  // [K][RS][C]
+  bf16* crsk;        // parity classes [C][Rc][Sc][K] back to back
+  int K, C, R, S, st, pad;
+  int cls_off[4];    // element offset of each stride-parity class
+  int ntk, ntc;      // 64-wide tiles of K and C
+};
+struct CJobs {
+  CJob j[24];
+  int start[25];
+  int njobs;
+  float* steps[80];  // step counters to increment (block 0)
+  int nsteps;
+};
+
+// one workgroup per (job, tap, k tile, c tile): 64 x 64 bf16 transpose through LDS
+__global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
+  __shared__ uint16_t tile[64][66];
+  const int b = blockIdx.x;
+  if (b == 0 && threadIdx.x < J.nsteps) *J.steps[threadIdx.x] += 1.f;
+  if (J.njobs == 0) return;
+  int ji = 0;
+  while (ji + 1 < J.njobs && b >= J.start[ji + 1]) ++ji;
+  if (b >= J.start[J.njobs]) return;
+  const CJob& jb = J.j[ji];
+  int local = b - J.start[ji];
+  const int RS = jb.R * jb.S;
+  const int tc = local % jb.ntc;
+  local /= jb.ntc;
+  const int tk = local % jb.ntk;
+  const int tap = local / jb.ntk;
+  const int r = tap / jb.S, s = tap - r * jb.S;
+  const int k0 = tk * 64, c0 = tc * 64;
+  // load krsc[k0 + kk][tap][c0 .. c0 + 63]: thread = (kk = tid / 4, 16 channels)
+  {
+    const int kk = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
+    const uint16_t* src = (const uint16_t*)jb.krsc + ((size_t)(k0 + kk) * RS + tap) * jb.C + c0 + cc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) tile[kk][cc + e] = src[e];
+  }
+  __syncthreads();
+  // parity class of this tap and its (t, u) inside the class
+  const int st = jb.st;
+  const int ph = ((r - jb.pad) % st + st) % st, pw = ((s - jb.pad) % st + st) % st;
+  const int cl = ph * st + pw;
+  const int r0 = (ph + jb.pad) % st, s0 = (pw + jb.pad) % st;
+  const int Rc = (jb.R - r0 + st - 1) / st, Sc = (jb.S - s0 + st - 1) / st;
+  const int t = (r - r0) / st, u = (s - s0) / st;
+  {
+    const int cc = threadIdx.x >> 2, kk = (threadIdx.x & 3) * 16;
+    uint16_t* dst = (uint16_t*)jb.crsk + jb.cls_off[cl] + (((size_t)(c0 + cc) * Rc + t) * Sc + u) * jb.K + k0 + kk;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dst[e] = tile[kk + e][cc];
+  }
+}
+
+}  // namespace optim
+}  // namespace sqr
+
+using namespace sqr;
+using namespace sqr::optim;
+
+extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2,
+                             double eps, void* stream) {
+  SQR_CHECK_ARG(params && nparams >= 0 && nparams <= 80, "adam_step: 0 <= nparams <= 80");
+  hipStream_t st = as_stream(stream);
+  size_t maxlds = 16;
+  CJobs cj;
+  cj.njobs = 0;
+  cj.nsteps = 0;
+  int cblocks = 0;
+  for (int i0 = 0; i0 < nparams; i0 += MAXJ) {
+    Jobs J;
+    J.lr = lr;
+    J.b1 = beta1;
+    J.b2 = beta2;
+    J.fb2 = (float)beta2;
+    J.eps = (float)eps;
+    J.omb1 = (float)(1.0 - beta1);
+    J.omb2 = (float)(1.0 - beta2);
+    J.njobs = 0;
+    int blocks = 0;
+    for (int i = i0; i < nparams && i < i0 + MAXJ; ++i) {
+      const sqr_adam_param& q = params[i];
+      SQR_CHECK_ARG(q.p && q.g && q.exp_avg && q.exp_avg_sq && q.step && q.n > 0 && q.n < (1ll << 31),
+                    "adam_step: parameter %d: null pointer or bad size", i);
+      Job& jb = J.j[J.njobs];
+      jb.p = q.p;
+      jb.g = q.g;
+      jb.m = q.exp_avg;
+      jb.v = q.exp_avg_sq;
+      jb.step = q.step;
+      jb.n = (int)q.n;
+      jb.krsc = (bf16*)q.w_krsc;
+      jb.K = jb.C = jb.RS = jb.Kp = 0;
+      int nb;
+      if (q.w_krsc) {
+        const sqr_conv_desc& d = q.desc;
+        SQR_CHECK_ARG(d.dtype == SQR_DTYPE_BF16 && (long long)d.K * d.C * d.R * d.S == q.n && d.stride <= 2,
+                      "adam_step: parameter %d: packing needs a bf16 descriptor matching the weight", i);
+        jb.K = d.K;
+        jb.C = d.C;
+        jb.RS = d.R * d.S;
+        int kp = jb.C * jb.RS;
+        if (d.C < 8) {
+          kp = 64;
+          while (kp < d.R * d.S * d.C) kp *= 2;
+        }
+        jb.Kp = kp;
+        SQR_CHECK_ARG((size_t)jb.C * jb.RS * 4 <= 64 * 1024, "adam_step: conv row too large for LDS");
+        maxlds = maxlds > (size_t)jb.C * jb.RS * 4 ? maxlds : (size_t)jb.C * jb.RS * 4;
+        nb = d.K;
+        if (q.w_crsk) {
+          SQR_CHECK_ARG(d.K % 64 == 0 && d.C % 64 == 0 && cj.njobs < 24,
+                        "adam_step: parameter %d: dgrad packing needs K, C multiples of 64", i);
+          CJob& c = cj.j[cj.njobs];
+          c.krsc = (const bf16*)q.w_krsc;
+          c.crsk = (bf16*)q.w_crsk;
+          c.K = d.K;
+          c.C = d.C;
+          c.R = d.R;
+          c.S = d.S;
+          c.st = d.stride;
+          c.pad = d.pad;
+          int off = 0;
+          for (int ph = 0; ph < d.stride; ++ph)
+            for (int pw = 0; pw < d.stride; ++pw) {
+              const int r0 = (ph + d.pad) % d.stride, s0 = (pw + d.pad) % d.stride;
+              const int rc = r0 < d.R ? (d.R - r0 + d.stride - 1) / d.stride : 0;
+              const int sc = s0 < d.S ? (d.S - s0 + d.stride - 1) / d.stride : 0;
+              c.cls_off[ph * d.stride + pw] = off;
+              off += d.C * rc * sc * d.K;
+            }
+          c.ntk = d.K / 64;
+          c.ntc = d.C / 64;
+          cj.start[cj.njobs] = cblocks;
+          cblocks += jb.RS * c.ntk * c.ntc;
+          ++cj.njobs;
+        }
+      } else {
+        nb = (int)((q.n + CHUNK - 1) / CHUNK);
+      }
+      J.start[J.njobs] = blocks;
+      blocks += nb;
+      ++J.njobs;
+      cj.steps[cj.nsteps++] = q.step;
+    }
+    J.start[J.njobs] = blocks;
+    hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), maxlds, st, J);
+    SQR_HIP_LAUNCH_CHECK("adam_kernel");
+  }
+  cj.start[cj.njobs] = cblocks;
+  const int cb = cblocks > 1 ? cblocks : 1;
+  hipLaunchKernelGGL(crsk_kernel, dim3(cb), dim3(256), 0, st, cj);
+  SQR_HIP_LAUNCH_CHECK("crsk_kernel");
+  return 0;
+}

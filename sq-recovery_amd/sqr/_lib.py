@@ -40,6 +40,12 @@ class SqrTailGrads(ctypes.Structure):
                 ("dbh", c_void_p * 4)]
 
 
+class SqrAdamParam(ctypes.Structure):
+    _fields_ = [("p", c_void_p), ("g", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("step", c_void_p), ("n", ctypes.c_longlong), ("desc", SqrConvDesc), ("w_krsc", c_void_p),
+                ("w_crsk", c_void_p)]
+
+
 # name -> (restype, argtypes); must mirror include/sqr.h exactly
 SIGNATURES = {
     "sqr_version": (c_int, []),
@@ -95,6 +101,8 @@ SIGNATURES = {
     "sqr_stem_fused_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                    c_void_p]),
+    "sqr_adam_step": (c_int, [ctypes.POINTER(SqrAdamParam), c_int, c_double, c_double, c_double, c_double,
+                              c_void_p]),
     "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p]),

@@ -97,35 +97,57 @@ def _alloc_packed(weight, dt, need_crsk):
     return krsc, crsk
 
 
+def _pack_key(w):
+    return (w._version, w.data_ptr())
+
+
+def packed_buffers(m, dtype):
+    """The module's persistent packed-weight buffers for `dtype` (allocated on first use):
+    (krsc, crsk); crsk is None for C < 8 (no backward-data for the im2col convs)."""
+    buf = m._wpack.get(dtype)
+    if buf is None:
+        krsc, crsk = _alloc_packed(m.weight, dtype, True)
+        buf = [None, krsc, crsk]
+        m._wpack[dtype] = buf
+    return buf[1], buf[2]
+
+
+def mark_packed(m, dtype):
+    """Record that the module's packed buffers for `dtype` hold its current weight (sqr.optim.Adam
+    writes them in the same kernels that update the weight)."""
+    m._wpack[dtype][0] = _pack_key(m.weight)
+
+
 def pack_all(convs, dtype):
-    """Pack the weights of several sqr Conv2d modules for `dtype` in one launch (called at the
-    start of a model forward; the model clears the modules' caches at its end, see clear_packed).
-    A module's forward uses its cache only if (weight._version, dtype, data_ptr) still match."""
+    """Bring the persistent packed weights of several sqr Conv2d modules up to date for `dtype` in
+    one launch (called at the start of a model forward).  A module is repacked only when its weight
+    changed since (torch version counter or storage), so after an sqr.optim.Adam step — which
+    packs in its own kernels — nothing is launched here."""
     jobs = []
     for m in convs:
         w = m.weight
-        key = (w._version, dtype, w.data_ptr())
-        krsc, crsk = _alloc_packed(w, dtype, True)
+        krsc, crsk = packed_buffers(m, dtype)
+        if m._wpack[dtype][0] == _pack_key(w):
+            continue
         K, C, R, S = w.shape
         d = _desc(1, C, R, R, K, R, S, m.stride[0], m.padding[0], dtype)
-        jobs.append((m, key, w.detach().float().contiguous(), d, krsc, crsk))
+        jobs.append((m, w.detach().float().contiguous(), d, krsc, crsk))
     for i in range(0, len(jobs), 20):
         chunk = jobs[i:i + 20]
         arr = (SqrPackJob * len(chunk))()
-        for j, (_, _, w, d, krsc, crsk) in enumerate(chunk):
+        for j, (_, w, d, krsc, crsk) in enumerate(chunk):
             arr[j].w_kcrs = w.data_ptr()
             arr[j].desc = d
             arr[j].w_krsc = krsc.data_ptr()
             arr[j].w_crsk = crsk.data_ptr() if crsk is not None else None
-        check(lib().sqr_conv2d_pack_weights(arr, len(chunk), stream_ptr(chunk[0][2].device)),
+        check(lib().sqr_conv2d_pack_weights(arr, len(chunk), stream_ptr(chunk[0][1].device)),
               "sqr_conv2d_pack_weights")
-    for m, key, w, d, krsc, crsk in jobs:
-        m._packed = (key, krsc, crsk, w)
+    for m, *_ in jobs:
+        mark_packed(m, dtype)
 
 
 def clear_packed(convs):
-    for m in convs:
-        m._packed = None
+    """(kept for API compatibility: packed weights are persistent per module and dtype)"""
 
 
 def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
@@ -269,14 +291,13 @@ class Conv2d(nn.Conv2d):
                 or self.stride[0] != self.stride[1] or self.padding[0] != self.padding[1]
                 or isinstance(self.padding, str)):
             raise ValueError("sqr Conv2d supports groups=1, dilation=1, symmetric stride/padding only")
-        self._packed = None  # ((weight version, dtype, ptr), krsc, crsk, fp32 source) from pack_all
+        self._wpack = {}  # dtype -> [key of the weight they hold, krsc, crsk] (pack_all / sqr.optim.Adam)
 
     def _cached(self, x):
         dt = compute_dtype(x) if x.is_cuda else None
-        if self._packed is not None and dt is not None:
-            key, krsc, crsk, _ = self._packed
-            if key == (self.weight._version, dt, self.weight.data_ptr()):
-                return (krsc, crsk)
+        buf = self._wpack.get(dt) if dt is not None else None
+        if buf is not None and buf[0] == _pack_key(self.weight):
+            return (buf[1], buf[2])
         return None
 
     def forward(self, x):

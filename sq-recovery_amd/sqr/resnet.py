@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from .bn import bn_act, count_batches, fused_stem, fused_stem_ok, stem
-from .conv import Conv2d, clear_packed, compute_dtype, pack_all
+from .conv import Conv2d, compute_dtype, pack_all
 
 
 class BasicBlock(nn.Module):
@@ -82,14 +82,11 @@ class ResNet18(nn.Module):
         if x.is_cuda:  # pack every conv weight of this step in one launch
             pack_all(convs, compute_dtype(x))
         count_batches([m for m in self.modules() if isinstance(m, nn.BatchNorm2d)])
-        try:
-            if fuse:
-                x = fused_stem(x, self.conv1, self.bn1, counted=True)
-            else:
-                x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
-            return self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        finally:
-            clear_packed(convs)  # packed weights live on in autograd's saved tensors only
+        if fuse:
+            x = fused_stem(x, self.conv1, self.bn1, counted=True)
+        else:
+            x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
+        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
 
     def forward(self, x):
         x = self.features(x)

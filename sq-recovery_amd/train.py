@@ -30,6 +30,7 @@ from classes import H5Dataset, ImplicitLoss, IoUAccuracy, SyntheticDataset  # no
 from helpers import load_model, parse_csv, save_compare_images, save_model  # noqa: E402
 from models import ResNetSQ  # noqa: E402
 from sqr import dist  # noqa: E402
+from sqr.optim import Adam  # noqa: E402
 
 
 def parse_args(argv=None):
@@ -79,7 +80,10 @@ def main(argv=None):
         dataset = H5Dataset(args.dataset_location, parse_csv(args.labels), train_split=0.9, dataset_file="dataset.h5")
 
     net = ResNetSQ(outputs=4, pretrained=bool(args.pretrained)).to(device)
-    optimizer = optim.Adam(net.parameters(), lr=args.lr, weight_decay=0)
+    # torch.optim.Adam semantics / state_dict on libsqr's fused step (+ bf16 conv weight packing)
+    optimizer = Adam(net.parameters(), lr=args.lr, weight_decay=0)
+    if args.bf16:
+        optimizer.attach(net)
     scheduler = optim.lr_scheduler.ReduceLROnPlateau(optimizer, patience=25)
     starting_epoch = 0
     if args.continue_training:
