@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline steps (0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="capture the whole train step in a HIP graph (1/0; default: on for 1 GPU)")
+                    help="capture the whole train step in a HIP graph (1/0; default: on)")
     args = ap.parse_args()
 
     from sqr import dist
@@ -93,14 +93,22 @@ def main():
     params = torch.tensor(classes.sample_sq_params(rng, B), device=dev)
     images = losses.implicit_render(params, H, 1.5, 260).unsqueeze(1).contiguous()  # [B,1,256,256] in [0,1]
 
-    torch.manual_seed(0)  # identical init on every rank (DDP also broadcasts)
+    torch.manual_seed(0)  # identical init on every rank (the data-parallel wrappers also broadcast)
     net = models.ResNetSQ(outputs=4, pretrained=False).to(dev)
     state0 = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
-    model = dist.wrap(net, dev)  # DDP (RCCL all-reduce overlapped with backward) when world > 1
-    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
     # torch.optim.Adam's semantics on libsqr's fused step (also writes the bf16 packed conv weights)
     opt = sqr_optim.Adam(net.parameters(), lr=1e-4, weight_decay=0).attach(net)
     crit = classes.ImplicitLoss(R, dev, 1.5, 260)
+    use_graph = args.graph != 0
+    # N > 1: the graph-captured data-parallel step (flat gradient buffer + one RCCL all-reduce in the
+    # graph) unless disabled; eager DDP (bucketed all-reduce overlapped with backward) otherwise
+    gdp = None
+    model = net
+    if world > 1 and use_graph and os.environ.get("SQR_DP_GRAPH", "1") == "1":
+        gdp = dist.GraphDataParallel(net, opt, dev)
+    elif world > 1:
+        model = dist.wrap(net, dev)
+        use_graph = False
 
     def body():
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -108,6 +116,8 @@ def main():
         pred = torch.cat([o.float() for o in out], dim=1)
         loss = crit(images, pred)
         loss.backward()
+        if gdp is not None:
+            gdp.allreduce()
         opt.step()
         return loss.detach()
 
@@ -117,13 +127,15 @@ def main():
 
     step = eager_step
     if use_graph:
-        # whole-step HIP graph: forward + fused loss + backward + Adam replayed as one launch
-        # (the libsqr kernels are enqueued on torch's current stream, so they are captured too)
+        # whole-step HIP graph: forward + fused loss + backward (+ all-reduce) + Adam replayed as one
+        # launch (the libsqr kernels are enqueued on torch's current stream, so they are captured too)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(3):
                 eager_step()
+                if gdp is not None:
+                    gdp.check_grads()
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
@@ -199,7 +211,9 @@ def main():
                       "model": "ResNetSQ (resnet18 backbone, 11.37M params)", "global_batch": B * world,
                       "per_gpu_batch": B, "image": "256x256x1", "render_size": R,
                       "parallelism": "dp%d" % world},
-           "mean_loss": mean_loss, "hip_graph": use_graph, "roofline": roof}
+           "mean_loss": mean_loss, "hip_graph": use_graph,
+           "dp": ("graph-captured RCCL all-reduce" if gdp is not None else ("DDP" if world > 1 else None)),
+           "roofline": roof}
 
     if rank == 0 and world == 1 and args.cpu_steps > 0:
         imgs_cpu = images.detach().cpu()

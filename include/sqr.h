@@ -222,7 +222,9 @@ int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int W, const fl
  * 80 fp32 parameters, fused with the bf16 packing of conv weights: when w_krsc is set (desc: the
  * conv geometry, dtype BF16) the updated weight is also written as sqr_conv2d_pack_weight's w_krsc
  * (and w_crsk when set; K, C multiples of 64).  step: the parameter's device step counter (float),
- * read as t = step + 1 for the bias corrections and incremented.  params is a host array. */
+ * read as t = step + 1 for the bias corrections and incremented.  grad_scale multiplies every
+ * gradient as it is read (1 = torch.optim.Adam; 1/N averages gradients all-reduced with SUM over N
+ * data-parallel ranks).  params is a host array. */
 typedef struct sqr_adam_param {
   float* p;
   const float* g;
@@ -235,7 +237,7 @@ typedef struct sqr_adam_param {
   void* w_crsk; /* nullable */
 } sqr_adam_param;
 int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2, double eps,
-                  void* stream);
+                  double grad_scale, void* stream);
 
 /* ---------------------------------------------------------------- ResNetSQ tail (fused) */
 

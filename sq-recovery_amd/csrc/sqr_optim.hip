@@ -41,6 +41,7 @@ struct Jobs {
   double lr, b1, b2;   // as torch's Python scalars
   float fb2, eps;
   float omb1, omb2;    // 1 - b1, 1 - b2 (computed in double, as torch does)
+  float gscale;        // gradients are used as g * gscale (1 = torch; 1/N averages summed data-parallel grads)
 };
 
 // torch's multi-tensor Adam, operation by operation (explicitly rounded: no fma contraction):
@@ -68,7 +69,7 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
     const int i1 = min(i0 + CHUNK, jb.n);
     for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) {
       float p = jb.p[i], m = jb.m[i], v = jb.v[i];
-      adam_update(p, m, v, jb.g[i], J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+      adam_update(p, m, v, J.gscale == 1.f ? jb.g[i] : jb.g[i] * J.gscale, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
       jb.p[i] = p;
       jb.m[i] = m;
       jb.v[i] = v;
@@ -80,7 +81,7 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   const size_t base = (size_t)k * CRS;
   for (int i = threadIdx.x; i < CRS; i += 256) {
     float p = jb.p[base + i], m = jb.m[base + i], v = jb.v[base + i];
-    adam_update(p, m, v, jb.g[base + i], J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+    adam_update(p, m, v, J.gscale == 1.f ? jb.g[base + i] : jb.g[base + i] * J.gscale, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
     jb.p[base + i] = p;
     jb.m[base + i] = m;
     jb.v[base + i] = v;
@@ -162,7 +163,7 @@ using namespace sqr;
 using namespace sqr::optim;
 
 extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2,
-                             double eps, void* stream) {
+                             double eps, double grad_scale, void* stream) {
   SQR_CHECK_ARG(params && nparams >= 0 && nparams <= 80, "adam_step: 0 <= nparams <= 80");
   hipStream_t st = as_stream(stream);
   size_t maxlds = 16;
@@ -179,6 +180,7 @@ extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double l
     J.eps = (float)eps;
     J.omb1 = (float)(1.0 - beta1);
     J.omb2 = (float)(1.0 - beta2);
+    J.gscale = (float)grad_scale;
     J.njobs = 0;
     int blocks = 0;
     for (int i = i0; i < nparams && i < i0 + MAXJ; ++i) {

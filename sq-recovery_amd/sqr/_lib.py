@@ -102,7 +102,7 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                    c_void_p]),
     "sqr_adam_step": (c_int, [ctypes.POINTER(SqrAdamParam), c_int, c_double, c_double, c_double, c_double,
-                              c_void_p]),
+                              c_double, c_void_p]),
     "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p]),

@@ -10,6 +10,7 @@ import ctypes
 
 import torch
 
+from . import gradbuf
 from ._lib import check, lib, ptr, stream_ptr
 
 _CL = torch.channels_last
@@ -63,6 +64,7 @@ class BNActFn(torch.autograd.Function):
                                    stream_ptr(x.device)), "sqr_bn_fwd")
         ctx.relu, ctx.training, ctx.eps = relu, training, eps
         ctx.has_res = residual is not None
+        ctx.pids = (id(weight), id(bias))
         if training:
             ctx.save_for_backward(x, mask, weight, mean, invstd)
         else:
@@ -84,8 +86,8 @@ class BNActFn(torch.autograd.Function):
             return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
-        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        dgamma = gradbuf.out(ctx.pids[0], (C,), x.device)
+        dbeta = gradbuf.out(ctx.pids[1], (C,), x.device)
         n = _ws_bytes(M, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
@@ -162,6 +164,7 @@ class StemFn(torch.autograd.Function):
                                      ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_stem_fwd")
         if not training:
             ctx.mark_non_differentiable(y)
+        ctx.pids = (id(weight), id(bias))
         ctx.save_for_backward(x, y, arg, weight, mean, invstd)
         return y
 
@@ -173,8 +176,8 @@ class StemFn(torch.autograd.Function):
         dy = dy.to(x.dtype).contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         dx = torch.empty_like(x, memory_format=_CL)
-        dgamma = torch.empty(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty(C, dtype=torch.float32, device=x.device)
+        dgamma = gradbuf.out(ctx.pids[0], (C,), x.device)
+        dbeta = gradbuf.out(ctx.pids[1], (C,), x.device)
         n = lib().sqr_stem_workspace_bytes(N, H, W, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         check(lib().sqr_stem_bwd(ptr(dy), ptr(y), ptr(arg), ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(mean),
@@ -224,6 +227,7 @@ class FusedStemFn(torch.autograd.Function):
         if not training:
             ctx.mark_non_differentiable(y)
         ctx.xdt = xdt
+        ctx.pids = (id(w), id(gamma), id(beta))
         ctx.save_for_backward(x, wf, gamma, y, arg, mean, invstd)
         return y
 
@@ -235,9 +239,9 @@ class FusedStemFn(torch.autograd.Function):
         N, _, H, W = x.shape
         dy = dy.to(torch.bfloat16).contiguous(memory_format=_CL)
         L = lib()
-        dw = torch.empty_like(wf)
-        dgamma = torch.empty(64, dtype=torch.float32, device=x.device)
-        dbeta = torch.empty(64, dtype=torch.float32, device=x.device)
+        dw = gradbuf.out(ctx.pids[0], tuple(wf.shape), x.device)
+        dgamma = gradbuf.out(ctx.pids[1], (64,), x.device)
+        dbeta = gradbuf.out(ctx.pids[2], (64,), x.device)
         n = L.sqr_stem_fused_workspace_bytes(N, H, W)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         check(L.sqr_stem_fused_bwd(ptr(x), ctx.xdt, N, H, W, ptr(wf), ptr(gamma), ptr(mean), ptr(invstd), ptr(dy),

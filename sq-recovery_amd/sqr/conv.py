@@ -11,6 +11,7 @@ Compute dtype: bfloat16 when the input is bf16 or CUDA autocast is on with bf16,
 import torch
 import torch.nn as nn
 
+from . import gradbuf
 from ._lib import SqrConvDesc, SqrPackJob, check, lib, ptr, stream_ptr
 
 DT_F32, DT_BF16 = 0, 1
@@ -190,10 +191,11 @@ def conv2d_bwd_data(gy, w_crsk, d):
     return dx
 
 
-def conv2d_bwd_weight(x, gy, d, col=None):
-    """dW (fp32, [K,C,R,S]); for C<8 convs pass the forward's workspace as `col` to skip im2col."""
+def conv2d_bwd_weight(x, gy, d, col=None, wid=None):
+    """dW (fp32, [K,C,R,S]); for C<8 convs pass the forward's workspace as `col` to skip im2col;
+    `wid` = id of the weight parameter (its sqr.gradbuf slot, if any, receives dW)."""
     import ctypes
-    dw = torch.empty((d.K, d.C, d.R, d.S), dtype=torch.float32, device=gy.device)
+    dw = gradbuf.out(wid, (d.K, d.C, d.R, d.S), gy.device)
     L = lib()
     n = L.sqr_conv2d_workspace_bytes(ctypes.byref(d), 2)
     if col is not None:
@@ -241,6 +243,7 @@ class Conv2dFn(torch.autograd.Function):
         if bias is not None:
             y = y + bias.to(dt).view(1, K, 1, 1)
         ctx.d = d
+        ctx.wid = id(weight)
         ctx.x_dtype = x.dtype
         ctx.has_bias = bias is not None
         need_w = ctx.needs_input_grad[1]
@@ -266,7 +269,7 @@ class Conv2dFn(torch.autograd.Function):
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
             dx = conv2d_bwd_data(g, crsk, d).to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
-            dw = conv2d_bwd_weight(xin, g, d, col)
+            dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
         return dx, dw, db, None, None, None, None, None

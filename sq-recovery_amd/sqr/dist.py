@@ -62,6 +62,49 @@ def wrap(model, device):
                broadcast_buffers=False)
 
 
+class GraphDataParallel:
+    """Data parallelism whose whole step — forward, loss, backward, gradient all-reduce, optimizer —
+    can be captured as ONE HIP graph (DDP's reducer cannot be captured, and eager launching of the
+    ~200-kernel step is host-bound).
+
+    Every parameter gradient of a libsqr model (ResNetSQ: convs, BatchNorm, stem, tail) is written by
+    its backward op straight into a slot of one flat fp32 buffer (sqr.gradbuf, in backward order);
+    ``allreduce()`` sums that buffer in place over the ranks with one RCCL call, and the fused
+    optimizer averages while it reads (``optimizer.sqr_grad_scale = 1 / world``).  Semantics are DDP's:
+    parameters and buffers are broadcast from rank 0 once, BatchNorm statistics stay per rank.
+    Gradients must be None before each backward (``zero_grad(set_to_none=True)``)."""
+
+    def __init__(self, model, optimizer, device):
+        from . import gradbuf
+        self.model = model
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        if self.world > 1:
+            with torch.no_grad():
+                for t in list(model.parameters()) + list(model.buffers()):
+                    dist.broadcast(t.data, 0)
+        self.flat = gradbuf.install(list(reversed(self.params)), device)
+        optimizer.sqr_grad_scale = 1.0 / self.world
+
+    def allreduce(self):
+        if dist.is_initialized():
+            dist.all_reduce(self.flat)  # SUM in place; the optimizer scales by 1 / world
+
+    def check_grads(self):
+        """Raise unless every parameter gradient is a view of the flat buffer (call after a backward)."""
+        lo = self.flat.data_ptr()
+        hi = lo + self.flat.numel() * self.flat.element_size()
+        for p in self.params:
+            if p.grad is None or not lo <= p.grad.data_ptr() < hi:
+                raise RuntimeError("GraphDataParallel: a parameter gradient was not produced by a libsqr op")
+
+    def close(self, optimizer=None):
+        from . import gradbuf
+        gradbuf.clear()
+        if optimizer is not None:
+            optimizer.sqr_grad_scale = 1.0
+
+
 def max_over_ranks(x):
     """max of a host float over all ranks (bench timing: the job is as slow as its slowest rank)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:

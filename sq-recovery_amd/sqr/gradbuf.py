@@ -1,0 +1,43 @@
+"""Parameter gradients written straight into one flat fp32 buffer (graph-captured data parallelism).
+
+For N > 1 GPUs the training step is captured as one HIP graph (sqr.dist.GraphDataParallel): the
+libsqr backward ops write each parameter's gradient directly into its slot of a flat buffer, so
+a single in-place RCCL all-reduce of that buffer (captured in the same graph) averages them — no
+DDP reducer (which cannot be captured), no bucket copies.  Autograd hands the slot view to
+``param.grad`` unchanged: it is a fresh, sole-owner, contiguous tensor, so AccumulateGrad keeps it
+instead of copying (grads must be None before backward: ``zero_grad(set_to_none=True)``).
+"""
+import torch
+
+_slots = {}  # id(param) -> (flat buffer, element offset, shape)
+
+
+def install(params, device):
+    """Allocate the flat buffer for `params` (in the given order) and register their slots.
+    Returns the buffer."""
+    params = list(params)
+    n = sum(p.numel() for p in params)
+    flat = torch.zeros(n, dtype=torch.float32, device=device)
+    off = 0
+    for p in params:
+        _slots[id(p)] = (flat, off, tuple(p.shape))
+        off += p.numel()
+    return flat
+
+
+def clear():
+    _slots.clear()
+
+
+def out(param_id, shape, device):
+    """A new view of the parameter's slot (or a plain new tensor when no buffer is installed)."""
+    s = _slots.get(param_id)
+    if s is None:
+        return torch.empty(shape, dtype=torch.float32, device=device)
+    flat, off, pshape = s
+    if tuple(shape) != pshape:
+        raise RuntimeError("sqr gradbuf: slot shape %s != gradient shape %s" % (pshape, tuple(shape)))
+    n = 1
+    for v in pshape:
+        n *= v
+    return flat.narrow(0, off, n).view(pshape)

@@ -28,6 +28,9 @@ class Adam(torch.optim.Adam):
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
                          capturable=True, **kw)
         self._convs = {}  # id(weight) -> (module, dtype)
+        # gradients are read as g * grad_scale (sqr.dist.GraphDataParallel sets 1/world after a SUM
+        # all-reduce; the fallback path requires 1)
+        self.sqr_grad_scale = 1.0
 
     def attach(self, model, dtype=torch.bfloat16):
         """Pack the conv weights of `model` (sqr Conv2d modules) for `dtype` inside every step."""
@@ -64,6 +67,9 @@ class Adam(torch.optim.Adam):
                 p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and not p.grad.is_sparse
                 and p.grad.dtype == torch.float32 and p.grad.is_contiguous() for p in ps)
             if not ok:
+                if self.sqr_grad_scale != 1.0:
+                    raise RuntimeError("sqr Adam: grad_scale != 1 needs the fused path (fp32 CUDA params, "
+                                       "weight_decay 0, no amsgrad/maximize)")
                 return super().step() if closure is None else (super().step(), loss)[1]
             groups.append((group, ps))
         L = lib()
@@ -93,7 +99,7 @@ class Adam(torch.optim.Adam):
                             a.w_crsk = crsk.data_ptr() if crsk is not None else None
                             packed.append((m, dt))
                 check(L.sqr_adam_step(arr, len(chunk), lr, float(b1), float(b2), float(group["eps"]),
-                                      stream_ptr(chunk[0].device)), "sqr_adam_step")
+                                      float(self.sqr_grad_scale), stream_ptr(chunk[0].device)), "sqr_adam_step")
                 for m, dt in packed:
                     mark_packed(m, dt)
         return loss

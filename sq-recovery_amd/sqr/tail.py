@@ -11,6 +11,7 @@ import ctypes
 
 import torch
 
+from . import gradbuf
 from ._lib import SqrTailDesc, SqrTailGrads, check, lib, ptr, stream_ptr
 
 _HEAD_N = (3, 2, 3, 4)
@@ -44,6 +45,7 @@ class TailFn(torch.autograd.Function):
         outs = [torch.empty(x.shape[0], n, dtype=torch.float32, device=x.device) for n in _HEAD_N]
         check(L.sqr_tail_fwd(ctypes.byref(d), ptr(x), *[ptr(o) for o in outs], ptr(save), stream_ptr(x.device)),
               "sqr_tail_fwd")
+        ctx.pids = tuple(id(p) for p in params)
         ctx.save_for_backward(x, save, *params)
         return tuple(outs)
 
@@ -66,7 +68,7 @@ class TailFn(torch.autograd.Function):
             g.g_out[i] = go.data_ptr()
             g.ld[i] = go.stride(0)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        grads = [torch.empty_like(p) for p in params]
+        grads = [gradbuf.out(i, tuple(p.shape), x.device) for i, p in zip(ctx.pids, params)]
         g.dx = dx.data_ptr()
         g.dw0, g.db0, g.dw1, g.db1 = (t.data_ptr() for t in grads[:4])
         for i in range(4):
