@@ -104,7 +104,11 @@ def main():
     # graph) unless disabled; eager DDP (bucketed all-reduce overlapped with backward) otherwise
     gdp = None
     model = net
-    if world > 1 and use_graph and os.environ.get("SQR_DP_GRAPH", "1") == "1":
+    force_dp = os.environ.get("SQR_DP_FORCE", "0") == "1"  # N=1 rehearsal of the N>1 path (world-1 RCCL group)
+    if force_dp and world == 1 and not torch.distributed.is_initialized():
+        torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get(
+            "MASTER_PORT", "29517"), rank=0, world_size=1, device_id=dev)
+    if (world > 1 or force_dp) and use_graph and os.environ.get("SQR_DP_GRAPH", "1") == "1":
         gdp = dist.GraphDataParallel(net, opt, dev)
     elif world > 1:
         model = dist.wrap(net, dev)

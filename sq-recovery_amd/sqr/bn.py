@@ -93,6 +93,7 @@ class BNActFn(torch.autograd.Function):
         check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
+        gradbuf.written(ctx.pids)
         if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
             dres = dy
         return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None
@@ -183,6 +184,7 @@ class StemFn(torch.autograd.Function):
         check(lib().sqr_stem_bwd(ptr(dy), ptr(y), ptr(arg), ptr(x), N, H, W, C, _dt(x), ptr(weight), ptr(mean),
                                  ptr(invstd), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n, stream_ptr(x.device)),
               "sqr_stem_bwd")
+        gradbuf.written(ctx.pids)
         return dx, dgamma, dbeta, None, None, None, None, None, None
 
 
@@ -247,6 +249,7 @@ class FusedStemFn(torch.autograd.Function):
         check(L.sqr_stem_fused_bwd(ptr(x), ctx.xdt, N, H, W, ptr(wf), ptr(gamma), ptr(mean), ptr(invstd), ptr(dy),
                                    ptr(y), ptr(arg), ptr(dw), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                    stream_ptr(x.device)), "sqr_stem_fused_bwd")
+        gradbuf.written(ctx.pids)
         return None, dw, dgamma, dbeta, None, None, None, None, None
 
 

@@ -270,6 +270,7 @@ class Conv2dFn(torch.autograd.Function):
             dx = conv2d_bwd_data(g, crsk, d).to(ctx.x_dtype)
         if ctx.needs_input_grad[1]:
             dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid)
+            gradbuf.written((ctx.wid,))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
         return dx, dw, db, None, None, None, None, None

@@ -68,13 +68,16 @@ class GraphDataParallel:
     ~200-kernel step is host-bound).
 
     Every parameter gradient of a libsqr model (ResNetSQ: convs, BatchNorm, stem, tail) is written by
-    its backward op straight into a slot of one flat fp32 buffer (sqr.gradbuf, in backward order);
-    ``allreduce()`` sums that buffer in place over the ranks with one RCCL call, and the fused
-    optimizer averages while it reads (``optimizer.sqr_grad_scale = 1 / world``).  Semantics are DDP's:
+    its backward op straight into a slot of one flat fp32 buffer (sqr.gradbuf, in backward order).
+    The buffer is cut into buckets of ~``bucket_mb``; as soon as the backward has enqueued the last
+    gradient of a bucket, that bucket is summed in place over the ranks by RCCL on a side stream,
+    overlapping the rest of the backward (the dependencies are stream events, so they are captured
+    with the graph).  ``allreduce()`` (after ``backward``) joins the side stream; the fused optimizer
+    averages while it reads (``optimizer.sqr_grad_scale = 1 / world``).  Semantics are DDP's:
     parameters and buffers are broadcast from rank 0 once, BatchNorm statistics stay per rank.
     Gradients must be None before each backward (``zero_grad(set_to_none=True)``)."""
 
-    def __init__(self, model, optimizer, device):
+    def __init__(self, model, optimizer, device, bucket_mb=BUCKET_MB):
         from . import gradbuf
         self.model = model
         self.world = dist.get_world_size() if dist.is_initialized() else 1
@@ -83,12 +86,63 @@ class GraphDataParallel:
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
                     dist.broadcast(t.data, 0)
-        self.flat = gradbuf.install(list(reversed(self.params)), device)
+        order = list(reversed(self.params))  # the backward produces the last layers' grads first
+        self.flat = gradbuf.install(order, device)
+        # buckets: contiguous ranges of the flat buffer
+        self.buckets, self.bucket_of, size, start, members = [], {}, 0, 0, []
+        cap = int(bucket_mb * 2 ** 20 / 4)
+        off = 0
+        for p in order:
+            members.append(id(p))
+            off += p.numel()
+            if off - start >= cap:
+                self.buckets.append((start, off, members))
+                start, members = off, []
+        if members:
+            self.buckets.append((start, off, members))
+        for b, (_, _, mem) in enumerate(self.buckets):
+            for pid in mem:
+                self.bucket_of[pid] = b
+        device = torch.device(device)
+        self.side = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self._reset()
+        gradbuf.set_listener(self._written)
         optimizer.sqr_grad_scale = 1.0 / self.world
 
+    def _reset(self):
+        self.pending = [len(mem) for _, _, mem in self.buckets]
+        self.launched = [False] * len(self.buckets)
+
+    def _launch(self, b):
+        if self.launched[b] or not dist.is_initialized():
+            self.launched[b] = True
+            return
+        self.launched[b] = True
+        lo, hi, _ = self.buckets[b]
+        view = self.flat[lo:hi]
+        if self.side is None:
+            dist.all_reduce(view)
+            return
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            dist.all_reduce(view)  # SUM in place; the optimizer scales by 1 / world
+
+    def _written(self, pids):
+        for pid in pids:
+            b = self.bucket_of.get(pid)
+            if b is None:
+                continue
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self._launch(b)
+
     def allreduce(self):
-        if dist.is_initialized():
-            dist.all_reduce(self.flat)  # SUM in place; the optimizer scales by 1 / world
+        """Finish the gradient all-reduce of this step (call after backward, before the optimizer)."""
+        for b in range(len(self.buckets)):
+            self._launch(b)  # buckets whose gradients were not all produced
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+        self._reset()
 
     def check_grads(self):
         """Raise unless every parameter gradient is a view of the flat buffer (call after a backward)."""

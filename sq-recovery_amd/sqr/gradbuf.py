@@ -10,6 +10,7 @@ instead of copying (grads must be None before backward: ``zero_grad(set_to_none=
 import torch
 
 _slots = {}  # id(param) -> (flat buffer, element offset, shape)
+_listener = [None]  # called with the ids of parameters whose gradients were just enqueued
 
 
 def install(params, device):
@@ -27,6 +28,18 @@ def install(params, device):
 
 def clear():
     _slots.clear()
+    _listener[0] = None
+
+
+def set_listener(fn):
+    _listener[0] = fn
+
+
+def written(param_ids):
+    """Backward ops call this right after enqueueing the kernels that write these gradients."""
+    fn = _listener[0]
+    if fn is not None:
+        fn(param_ids)
 
 
 def out(param_id, shape, device):

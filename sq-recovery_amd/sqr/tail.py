@@ -79,6 +79,7 @@ class TailFn(torch.autograd.Function):
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         check(L.sqr_tail_bwd(ctypes.byref(d), ptr(save), ctypes.byref(g), ptr(ws), n, stream_ptr(x.device)),
               "sqr_tail_bwd")
+        gradbuf.written(ctx.pids)
         # a head whose output received no gradient gets None (as autograd would give it), not zeros
         for i, go in enumerate(gouts):
             if go is None:

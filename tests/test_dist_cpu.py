@@ -84,6 +84,27 @@ def _worker(rank, world, port, tmpdir, q):
             fresh = ref_torch.ResNetSQRef()
             fresh.load_state_dict(ck["model_state_dict"])
             res["epoch"] = ck["epoch"]
+        # GraphDataParallel plumbing (the N-GPU graph path of bench.py): broadcast from rank 0, the
+        # flat gradient buffer, one SUM all-reduce, averaging scale handed to the optimizer
+        from sqr import gradbuf
+
+        class _Opt:
+            sqr_grad_scale = 1.0
+        torch.manual_seed(100 + rank)  # different init per rank: the broadcast must equalise it
+        m2 = ref_torch.ResNetSQRef()
+        opt2 = _Opt()
+        gdp = sd.GraphDataParallel(m2, opt2, dev)
+        res["bcast_sum"] = float(sum(p.double().sum() for p in m2.parameters()))
+        res["scale"] = opt2.sqr_grad_scale
+        for i, p in enumerate(gdp.params):
+            gradbuf.out(id(p), tuple(p.shape), dev).fill_(float(rank + 1) * (i + 1))
+        gradbuf.written([id(p) for p in gdp.params[: len(gdp.params) // 2]])  # some buckets complete early
+        res["nbuckets"] = len(gdp.buckets)
+        gdp.allreduce()
+        res["flat_ok"] = all(
+            torch.all(gradbuf.out(id(p), tuple(p.shape), dev) == 3.0 * (i + 1)).item()
+            for i, p in enumerate(gdp.params))
+        gdp.close(opt2)
         sd.barrier()
         sd.finish()
         q.put((rank, res))
@@ -126,3 +147,7 @@ def test_ddp_gloo_world2(tmp_path):
     for r in range(world):
         assert out[r]["grad_rel_err"] < 1e-5, out[r]["grad_rel_err"]
     assert out[0]["keys_prefixed"] is False and out[0]["epoch"] == 3
+    assert out[0]["bcast_sum"] == out[1]["bcast_sum"]
+    assert out[0]["scale"] == out[1]["scale"] == 0.5
+    assert out[0]["flat_ok"] and out[1]["flat_ok"]
+    assert out[0]["nbuckets"] >= 2
