@@ -27,6 +27,7 @@
 // Convs whose input has < 8 channels (conv1: C=1) run as an explicit im2col (K padded to 64) +
 // 1x1 GEMM through the same kernels.
 #include <stdint.h>
+#include <stdlib.h>
 #include "sqr_conv_dev.h"
 
 namespace sqr {
@@ -88,15 +89,17 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_row_block) {
 // tiles kt+1..kt+STAGES-1 stay in flight across the raw s_barrier; a counted s_waitcnt vmcnt
 // retires exactly the tile read next.
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int STAGES>
-__global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti mc) {
   using C = Cfg<T>;
   constexpr int BK = 128 / C::ES;  // k elements per LDS row (128 B)
   constexpr int ROWB = 128;
+  constexpr int NW = WAVES_M * WAVES_N, NT = 64 * NW;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int QV = BM / 32, PV = BN / 32;  // glds per wave per tile for Q / P
+  constexpr int QV = BM / (8 * NW), PV = BN / (8 * NW);  // glds per wave per tile for Q / P
   constexpr int PER_TILE = QV + PV;
-  static_assert(WAVES_M * WAVES_N == 4, "4 waves");
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(QV >= 1 && PV >= 1 && QV * 8 * NW == BM && PV * 8 * NW == BN, "tile rows per wave");
   constexpr int TILE_Q = BM * ROWB, TILE_P = BN * ROWB, STAGE = TILE_Q + TILE_P;
   // ONE __shared__ array, no other LDS reads in the loop: an LDS read that may alias an in-flight
   // LDS-DMA makes hipcc insert s_waitcnt vmcnt(0) in front of it (that killed the pipeline when
@@ -116,7 +119,8 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
   const int tile_m = bid / a.ntn, tile_n = bid % a.ntn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  // this lane's rows: r_i = 8*(4i + wave) + (lane>>3); its logical slot is the same for every i.
+  // this lane's rows: r_i = 8*(NW*i + wave) + (lane>>3); its logical slot is the same for every i
+  // (NW even: the row swizzle (r>>1)&7 = (4*wave + (lane>>4))&7).
   // Loads go through buffer descriptors: an out-of-range voffset returns zeros, so padding /
   // out-of-tensor lanes just get voffset = kOOB and the per-row work is a few 32-bit VALU ops.
   constexpr uint32_t kOOB = 0x80000000u;
@@ -125,7 +129,7 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
   int q_off[QV], q_hb[QV], q_wb[QV];
 #pragma unroll
   for (int i = 0; i < QV; ++i) {
-    const int m = m0 + 8 * (4 * i + wave) + lrow;
+    const int m = m0 + 8 * (NW * i + wave) + lrow;
     if (m < g.M) {
       const int n = (int)fdiv((uint32_t)m, g.fd_hw);
       const int rem = m - n * g.Ho * g.Wo;
@@ -142,7 +146,7 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
   uint32_t p_off[PV];
 #pragma unroll
   for (int i = 0; i < PV; ++i) {
-    const int n = n0 + 8 * (4 * i + wave) + lrow;
+    const int n = n0 + 8 * (NW * i + wave) + lrow;
     p_off[i] = n < a.Nout ? (uint32_t)(n * a.Kg * C::ES) : kOOB;
   }
   const __amdgpu_buffer_rsrc_t qsrd = __builtin_amdgcn_make_buffer_rsrc((void*)g.base, 0, g.bytes, 0x00020000);
@@ -150,31 +154,35 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
       __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, (uint32_t)(a.Nout * a.Kg * C::ES), 0x00020000);
   const int RS = g.R * g.S;
   const int nkt = (a.Kg + BK - 1) / BK;
+  // the loop's scalars as locals: read through `a`/`g` (a dynamically indexed kernel argument) they
+  // were re-loaded with s_load + s_waitcnt lgkmcnt(0) in every k step (the asm "memory" clobbers)
+  const int gHi = g.Hi, gWi = g.Wi, gCi = g.Ci, glog2Ci = g.log2Ci, gS = g.S, gks = g.ks, Kg = a.Kg;
+  const FastDiv fds = g.fd_s;
 
   auto issue = [&](int kt, int stage) {
     char* q = smem + stage * STAGE;
     char* p = q + TILE_Q;
     const int k = kt * BK + lslot * C::VEC;
-    const int tap = k >> g.log2Ci;
-    const int c = k & (g.Ci - 1);
+    const int tap = k >> glog2Ci;
+    const int c = k & (gCi - 1);
     const bool tap_ok = tap < RS;
-    const int tr = (int)fdiv((uint32_t)tap, g.fd_s);
-    const int dh = tr * g.ks, dw = (tap - tr * g.S) * g.ks;
-    const int tapoff = ((dh * g.Wi + dw) * g.Ci + c) * C::ES;
+    const int tr = (int)fdiv((uint32_t)tap, fds);
+    const int dh = tr * gks, dw = (tap - tr * gS) * gks;
+    const int tapoff = ((dh * gWi + dw) * gCi + c) * C::ES;
 #pragma unroll
     for (int i = 0; i < QV; ++i) {
       const int h = q_hb[i] + dh, w = q_wb[i] + dw;
-      const bool ok = tap_ok && (unsigned)h < (unsigned)g.Hi && (unsigned)w < (unsigned)g.Wi;
+      const bool ok = tap_ok && (unsigned)h < (unsigned)gHi && (unsigned)w < (unsigned)gWi;
       const uint32_t voff = ok ? (uint32_t)(q_off[i] + tapoff) : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qsrd, (__attribute__((address_space(3))) void*)(q + (8 * (4 * i + wave)) * ROWB),
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qsrd, (__attribute__((address_space(3))) void*)(q + (8 * (NW * i + wave)) * ROWB),
                                                16, voff, 0, 0, 0);
     }
     const uint32_t kb = (uint32_t)(k * C::ES);
-    const bool k_ok = k < a.Kg;
+    const bool k_ok = k < Kg;
 #pragma unroll
     for (int i = 0; i < PV; ++i) {
       const uint32_t voff = k_ok ? p_off[i] + kb : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(psrd, (__attribute__((address_space(3))) void*)(p + (8 * (4 * i + wave)) * ROWB),
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(psrd, (__attribute__((address_space(3))) void*)(p + (8 * (NW * i + wave)) * ROWB),
                                                16, voff, 0, 0, 0);
     }
   };
@@ -312,7 +320,7 @@ __global__ void __launch_bounds__(256) conv_nt_kernel(NTMulti mc) {
       }
     }
     __syncthreads();
-    for (int t = tid; t < BN; t += 256) {
+    for (int t = tid; t < BN; t += NT) {
       float a1 = 0.f, a2 = 0.f;
 #pragma unroll
       for (int w = 0; w < WAVES_M; ++w) {
@@ -828,23 +836,38 @@ Gather make_gather(const void* base, int Hi, int Wi, int Ci, int Ho, int Wo, int
   return g;
 }
 
-int nt_cfg(int M, int N) {
+int nt_cfg(int M, int N, bool bf16) {
   auto nblk = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   if (N >= 128 && nblk(128, 128) >= 512) return 0;
+  // one 128x128 tile per CU: 8 waves + a 4-deep ring (ResNetSQ layer3 convs, layer4's strided
+  // dgrad: 8-13 % faster than 128x64 / 4 waves, measured scratch/nt_tune.py)
+  if (bf16 && N >= 128 && nblk(128, 128) >= 256) return 5;
   if (nblk(128, 64) >= 512) return 1;
   if (N >= 128 && nblk(64, 128) >= 512) return 2;
   return 3;
 }
 
+// tile configs of launch_nt: BM, BN, threads
+const int kNtBM[8] = {128, 128, 64, 64, 256, 128, 128, 128};
+const int kNtBN[8] = {128, 64, 128, 64, 128, 128, 128, 64};
+const int kNtThreads[8] = {256, 256, 256, 256, 512, 512, 256, 512};
+
+int nt_pick(int M, int N, bool bf16) {
+  int cfg = nt_cfg(M, N, bf16);
+  if (const char* e = getenv("SQR_NT_CFG")) cfg = atoi(e);  // experiments: force a tile config
+  return cfg < 0 || cfg > 7 ? 0 : cfg;
+}
+
 // one launch for ncls NT GEMMs of the same output width (tile config from their total M)
 template <typename T>
 int launch_nt(NTArgs* cl, int ncls, hipStream_t st) {
-  // tile choice: biggest tile that still gives >= 2 workgroups per CU (512), else the smallest
+  // tile choice: biggest tile that still gives >= 2 workgroups per CU (512), one 8-wave 128x128 tile
+  // per CU, else the smallest
   int M = 0;
   for (int i = 0; i < ncls; ++i) M += cl[i].g.M;
   const int N = cl[0].Nout;
-  const int cfg = nt_cfg(M, N);
-  int bm = (cfg == 0 || cfg == 1) ? 128 : 64, bn = (cfg == 0 || cfg == 2) ? 128 : 64;
+  const int cfg = nt_pick(M, N, sizeof(T) == 2);
+  const int bm = kNtBM[cfg], bn = kNtBN[cfg];
   NTMulti mc;
   int total = 0;
   for (int i = 0; i < ncls; ++i) {
@@ -856,13 +879,17 @@ int launch_nt(NTArgs* cl, int ncls, hipStream_t st) {
   }
   for (int i = ncls; i < 4; ++i) mc.start[i] = total;
   mc.ncls = ncls;
-  const dim3 grid(total), blk(256);
+  const dim3 grid(total), blk(kNtThreads[cfg]);
   probe_begin(st);
   switch (cfg) {
     case 0: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, mc); break;
     case 1: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 64, 4, 1, 3>), grid, blk, 0, st, mc); break;
     case 2: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 128, 1, 4, 3>), grid, blk, 0, st, mc); break;
-    default: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, mc); break;
+    case 3: hipLaunchKernelGGL((conv_nt_kernel<T, 64, 64, 2, 2, 3>), grid, blk, 0, st, mc); break;
+    case 4: hipLaunchKernelGGL((conv_nt_kernel<T, 256, 128, 4, 2, 3>), grid, blk, 0, st, mc); break;
+    case 5: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 4, 4>), grid, blk, 0, st, mc); break;
+    case 6: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 128, 2, 2, 4>), grid, blk, 0, st, mc); break;
+    default: hipLaunchKernelGGL((conv_nt_kernel<T, 128, 64, 4, 2, 5>), grid, blk, 0, st, mc); break;
   }
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv_nt_kernel");
@@ -993,7 +1020,10 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
     if (rc != 1) return rc;  // launched (0) or failed; 1 = shape not covered by the direct kernel
   }
   a.stats = stats;
-  if (stats_rows) *stats_rows = (sh.M + ((nt_cfg(sh.M, d->K) <= 1) ? 128 : 64) - 1) / ((nt_cfg(sh.M, d->K) <= 1) ? 128 : 64);
+  if (stats_rows) {  // one partial row per M tile of the config launch_nt will pick
+    const int bm = kNtBM[nt_pick(sh.M, d->K, d->dtype == SQR_DTYPE_BF16)];
+    *stats_rows = (sh.M + bm - 1) / bm;
+  }
   if (sh.im2col) {
     const size_t need = sqr_conv2d_workspace_bytes(d, 0);
     if (workspace_bytes < need || !workspace) {
