@@ -39,6 +39,7 @@ def test_graph_dp_world1(tmp_path):
     from sqr import gradbuf, losses
     tdist.init_process_group("nccl", init_method="file://%s" % (tmp_path / "store"), rank=0, world_size=1,
                              device_id=torch.device(DEV))
+    g = None
     try:
         rng = np.random.default_rng(0)
         p = torch.tensor(classes.sample_sq_params(rng, 8), device=DEV)
@@ -73,4 +74,6 @@ def test_graph_dp_world1(tmp_path):
             assert (pa - pb).abs().max().item() <= 1e-5 * max(pa.abs().max().item(), 1e-3)
     finally:
         gradbuf.clear()
+        torch.cuda.synchronize()
+        del g  # the graph holds captured RCCL work: release it before the communicator
         tdist.destroy_process_group()
