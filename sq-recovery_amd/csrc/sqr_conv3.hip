@@ -21,7 +21,9 @@
 #include "sqr_conv_dev.h"
 
 #ifndef SQR_EXP
-#define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop)
+#define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop;
+                   // conv3_kernel: 4 no per-tap wait/barrier, 8 no MFMA, 16 no fragment reads;
+                   // conv3p_kernel: 32 no output / statistics stores, 64 no tap loop)
 #endif
 
 namespace sqr {
@@ -52,17 +54,11 @@ __device__ __forceinline__ void dma_pieces(__amdgpu_buffer_rsrc_t srd, char* dst
 
 // BatchNorm partials of a BM x BN output tile held as acc[j][i] (lane: pixel 16i+fr of its wave
 // rows, channels 16j+4fq..+3 of its wave columns), from the bf16 values actually stored.
-// Per-lane sums over i, then an LDS transpose: red[wave-row group][fr][col] -> one thread per
-// column adds its 16*WAVES_M partials in a fixed order (deterministic, no cross-lane shuffles).
-template <int BN, int WAVES_M, int WAVES_N, int TM, int TN, int NT>
-__device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* red, int wm, int wn, int fr, int fq,
-                                           int tid, float* stats_row0, float* stats_row1) {
-  constexpr int WN = BN / WAVES_N;
-  float s1[TN][4], s2[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
+// Per-lane sums over i (stats_accum), then an LDS transpose (stats_reduce): red[wave-row
+// group][fr][col] -> one thread per column adds its 16*WAVES_M partials in a fixed order
+// (deterministic, no cross-lane shuffles).
+template <int TM, int TN>
+__device__ __forceinline__ void stats_accum(const uint32_t (*pk)[TM][2], float (*s1)[4], float (*s2)[4]) {
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -75,6 +71,12 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
         s1[j][2 * h + 1] += hi;
         s2[j][2 * h + 1] = fmaf(hi, hi, s2[j][2 * h + 1]);
       }
+}
+
+template <int BN, int WAVES_M, int WAVES_N, int TN, int NT>
+__device__ __forceinline__ void stats_reduce(const float (*s1)[4], const float (*s2)[4], float* red, int wm, int wn,
+                                             int fr, int fq, int tid, float* stats_row0, float* stats_row1) {
+  constexpr int WN = BN / WAVES_N;
   // red: [2][WAVES_M*16 rows][BN cols] floats
   float* r1 = red + (wm * 16 + fr) * BN + wn * WN + 4 * fq;
   float* r2 = r1 + WAVES_M * 16 * BN;
@@ -92,6 +94,20 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
     for (int r = 0; r < WAVES_M * 16; ++r) acc += src[r * BN];
     (q ? stats_row1 : stats_row0)[col] = acc;
   }
+}
+
+// BatchNorm partials of a BM x BN output tile held as acc[j][i] (lane: pixel 16i+fr of its wave
+// rows, channels 16j+4fq..+3 of its wave columns), from the bf16 values actually stored.
+template <int BN, int WAVES_M, int WAVES_N, int TM, int TN, int NT>
+__device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* red, int wm, int wn, int fr, int fq,
+                                           int tid, float* stats_row0, float* stats_row1) {
+  float s1[TN][4], s2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
+  stats_accum<TM, TN>(pk, s1, s2);
+  stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(s1, s2, red, wm, wn, fr, fq, tid, stats_row0, stats_row1);
 }
 
 template <int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB>
@@ -204,15 +220,33 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         bf16x8 pf[TN], qf[TM];
+#if SQR_EXP & 16
+#pragma unroll
+        for (int j = 0; j < TN; ++j) pf[j] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)poff[j], 0u, 0u, (uint32_t)sub});
+#pragma unroll
+        for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)qoff[i], 0u, 0u, 0u});
+#else
 #pragma unroll
         for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(bst + (poff[j] ^ (sub << 6)));
 #pragma unroll
         for (int i = 0; i < TM; ++i) qf[i] = *(const bf16x8*)(win + (qoff[i] ^ (sub << 6)));
+#endif
+#if SQR_EXP & 8
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[j][i][0] += __builtin_bit_cast(float, (uint32_t)(__builtin_bit_cast(u32x4, pf[j])[0] ^ __builtin_bit_cast(u32x4, qf[i])[0]));
+#else
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
+#endif
       }
+#if SQR_EXP & 4
+      if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      continue;
+#endif
       // retire the weight tile of the next step (and at tap 8 the next window, which is older);
       // at taps 0-1 the next chunk's window is younger than it and stays in flight
       if (!more) {
@@ -253,6 +287,209 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
                                                  a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
 }
 
+
+// ============================================================================ layer-1 persistent
+// Cin = Nout = 64, W = 64 (ResNetSQ layer1, forward and backward-data): one workgroup per CU keeps
+// the whole 3x3 weight tensor (9 x 64 x 64 bf16 = 72 KiB) resident in LDS and walks 128-pixel
+// tiles (2 image rows of one image).  The halo window of its next tile streams in by LDS-DMA while
+// the current tile computes, and the current tile's output stores drain while the next one
+// computes (they are issued after the wait for the next window).  Two barriers per tile instead of
+// one per tap; no weight traffic after the first tile.
+struct D3PArgs {
+  const void* x;   // [N][H][64][64]
+  const void* w;   // [64][9][64]
+  void* out;       // [N][H][64][64]
+  float* stats;    // nullable: BatchNorm partials [ntiles][2][64]
+  int H, ntiles, flip;
+  uint32_t xbytes, wbytes;
+};
+
+__global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
+  constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
+  constexpr int WAVES_M = 2, WAVES_N = 2, WM = 64, WN = 32, TM = WM / 16, TN = WN / 16;
+  constexpr int WWID = TW + 2, WR = (TH + 2) * WWID;  // 264 halo-window rows
+  constexpr int WP = (WR + 8 * NW - 1) / (8 * NW);    // 9 window pieces per wave
+  constexpr int WIN = WP * 8 * NW * ROWB;             // 36 KiB per window buffer
+  constexpr int WPW = 9 * BN / (8 * NW);              // 18 weight pieces per wave
+  constexpr int WB = 9 * BN * ROWB;                   // 72 KiB: LDS row (tap, n)
+  constexpr int STG = TH * TW * BN * 2;                // 16 KiB staged output tile
+  constexpr int NST = STG / 16 / NT;                  // 16-B stores per thread per tile
+  static_assert(2 * WAVES_M * 16 * BN * 4 <= WIN, "statistics scratch fits a window buffer");
+  __shared__ __attribute__((aligned(1024))) char smem[WB + 2 * WIN + STG];  // 160 KiB
+  char* const wl = smem;
+  char* const winb = smem + WB;
+  char* const stg = winb + 2 * WIN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int prow = lane >> 3, pslot = lane & 7;
+  constexpr uint32_t kOOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, a.wbytes, 0x00020000);
+  const int H = a.H, tiles_per_img = H / TH;
+
+  {  // resident weights: LDS row r = tap * 64 + n  <-  w[n][tap][0..63]
+    uint32_t wv[WPW];
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      const int r = (i * NW + wave) * 8 + prow;
+      const int tap = r / BN, n = r - tap * BN;
+      wv[i] = (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4));
+    }
+    dma_pieces<WPW, NW>(wsrd, wl, wv, 0, wave);
+  }
+  auto issue_window = [&](int tile, char* dst) {
+    const int img = tile / tiles_per_img, h0 = (tile - img * tiles_per_img) * TH;
+    uint32_t vo[WP];
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int r = (i * NW + wave) * 8 + prow;
+      const int wy = r / WWID, wx = r - wy * WWID;
+      const int h = h0 - 1 + wy, w = wx - 1;
+      const bool ok = r < WR && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)TW;
+      vo[i] = ok ? (uint32_t)((((img * H + h) * TW + w) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4)) : kOOB;
+    }
+    dma_pieces<WP, NW>(xsrd, dst, vo, 0, wave);
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  int qbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wm * WM + 16 * i + fr;
+    qbase[i] = (m / TW) * WWID + (m % TW);
+  }
+  int poff[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int row = wn * WN + 16 * j + fr;
+    poff[j] = row * ROWB + ((fq ^ ((row >> 1) & 7)) << 4);
+  }
+  const int flip = a.flip;
+
+  const int G = gridDim.x;
+  int tile = xcd_remap(blockIdx.x, G);  // an XCD's workgroups walk neighbouring tiles together
+  if (tile < a.ntiles) issue_window(tile, winb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // BatchNorm partials accumulate over all of this workgroup's tiles: one partial row per workgroup
+  float st1[TN][4], st2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st1[j][e] = st2[j][e] = 0.f;
+  // the previous tile's output leaves the staging area right after the next window's DMA is issued,
+  // so the wait for that window (vmcnt(NST)) never waits for output stores
+  auto store_staged = [&](int t) {
+    const int img = t / tiles_per_img, h0 = (t - img * tiles_per_img) * TH;
+    char* __restrict__ dst = (char*)a.out + ((size_t)img * H + h0) * TW * BN * 2;
+#pragma unroll
+    for (int k = 0; k < NST; ++k) {
+      const int c = k * NT + tid, row = c >> 3, slot = c & 7;
+      const u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
+      *(u32x4*)(dst + (size_t)c * 16) = v;
+    }
+  };
+  int buf = 0, prev = -1;
+  for (; tile < a.ntiles; tile += G) {
+    const char* win = winb + buf * WIN;
+    if (tile + G < a.ntiles) issue_window(tile + G, winb + (buf ^ 1) * WIN);
+    if (prev >= 0) store_staged(prev);
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 18 (tap, k-half) steps, fragments software-pipelined one step ahead (one wave per SIMD:
+    // nothing else hides the LDS read latency)
+    auto load = [&](int s, bf16x8* pf, bf16x8* qf) {
+      const int t = s >> 1, sub = s & 1;
+      const int r = t / 3, c3 = t % 3;
+      const int toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
+      const char* wt = wl + t * BN * ROWB;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(wt + (poff[j] ^ (sub << 6)));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = qbase[i] + toff;
+        qf[i] = *(const bf16x8*)(win + ((row * ROWB + ((fq ^ ((row >> 1) & 7)) << 4)) ^ (sub << 6)));
+      }
+    };
+    auto mma = [&](const bf16x8* pf, const bf16x8* qf) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
+    };
+    bf16x8 pA[TN], qA[TM], pB[TN], qB[TM];
+    load(0, pA, qA);
+#if SQR_EXP & 64
+    if (a.ntiles < 0)
+#endif
+#pragma unroll
+    for (int s = 0; s < 18; s += 2) {
+      load(s + 1, pB, qB);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads a whole step ahead of their MFMAs
+      mma(pA, qA);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 2 < 18) load(s + 2, pA, qA);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(pB, qB);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t pk[TN][TM][2];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const bf16x2 lo = {(bf16)acc[j][i][0], (bf16)acc[j][i][1]};
+        const bf16x2 hi = {(bf16)acc[j][i][2], (bf16)acc[j][i][3]};
+        pk[j][i][0] = __builtin_bit_cast(uint32_t, lo);
+        pk[j][i][1] = __builtin_bit_cast(uint32_t, hi);
+      }
+    stats_accum<TM, TN>(pk, st1, st2);
+    // the next window has landed (only the NST younger output stores may still be in flight);
+    // after the barrier every wave is done with this window and with the staged previous tile
+    if (prev >= 0) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+#if SQR_EXP & 32
+    if (pk[0][0][0] == 0x12345678u) a.stats[tid] = 0.f;
+    buf ^= 1;
+    continue;
+#endif
+    // stage the 128 x 64 bf16 output tile (16 KiB, contiguous in NHWC); it is written back with
+    // 16-B per lane fully coalesced stores.  Row key (r ^ r>>3) & 7 on the 16-B slot: conflict-free
+    // reads, no 2-way write conflicts.
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = wm * WM + 16 * i + fr;
+      const int key = (m ^ (m >> 3)) & 7;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = wn * WN + 16 * j + 4 * fq;
+        *(u32x2*)(stg + m * ROWB + ((((n >> 3) ^ key) << 4) | ((n & 7) << 1))) = u32x2{pk[j][i][0], pk[j][i][1]};
+      }
+    }
+    __builtin_amdgcn_s_barrier();  // staged tile visible (LDS writes are waited by the barrier's lgkmcnt)
+    prev = tile;
+    buf ^= 1;
+  }
+  if (prev >= 0) store_staged(prev);
+  if (a.stats) {
+    __syncthreads();
+    stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(st1, st2, (float*)winb, wm, wn, fr, fq, tid,
+                                              a.stats + (size_t)blockIdx.x * 2 * BN,
+                                              a.stats + ((size_t)blockIdx.x * 2 + 1) * BN);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // ============================================================================ weight gradient
 // dW[k][tap][c] = sum_p dY[p][k] * X[p + shift(tap)][c] over the pixels of the split.  A
@@ -490,6 +727,7 @@ struct D3Cfg {
 };
 
 int g_direct = 1;  // 0 off, 1 on when the grid is big enough, 2 whenever the shape fits
+int g_persist = 1;  // layer-1 persistent kernel (0: the tiled conv3_kernel; tests compare the two)
 
 int pow2_log(int x) {
   int l = 0;
@@ -531,6 +769,31 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
   if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return 1;
   const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
   if (xbytes >= (1u << 31) || wbytes >= (1u << 31) || (size_t)N * H * W * Nout * 2 >= (1u << 31)) return 1;
+  if (Cin == 64 && Nout == 64 && W == 64 && H % 2 == 0 && g_persist) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    }
+    D3PArgs p;
+    p.x = x;
+    p.w = w;
+    p.out = out;
+    p.stats = stats;
+    p.H = H;
+    p.ntiles = N * (H / 2);
+    p.flip = flip;
+    p.xbytes = (uint32_t)xbytes;
+    p.wbytes = (uint32_t)wbytes;
+    const int grid = p.ntiles < ncu ? p.ntiles : ncu;
+    if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
+    probe_begin(st);
+    hipLaunchKernelGGL(conv3p_kernel, dim3(grid), dim3(256), 0, st, p);
+    probe_end(st);
+    SQR_HIP_LAUNCH_CHECK("conv3p_kernel");
+    return 0;
+  }
   D3Cfg c;
   if (!pick(N, H, W, Cin, Nout, &c)) return 1;
   D3Args a;

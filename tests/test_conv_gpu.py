@@ -120,7 +120,8 @@ def test_conv_deterministic():
 # Cin != Nout); forced on (mode 2) so the small test batches take it, and compared with the
 # implicit-GEMM path (mode 0) and the float64 reference
 DIRECT = [
-    (2, 64, 64, 64),     # cfg 0 (TW 64 x TH 4, single window)
+    (2, 64, 64, 64),     # layer-1 persistent kernel (resident weights), one tile per workgroup
+    (20, 64, 64, 64),    # persistent, several tiles per workgroup (640 tiles > CUs)
     (1, 64, 128, 64),    # cfg 0, two tiles per image row
     (2, 128, 32, 128),   # cfg 1 (TW 32 x TH 8, double-buffered window, 2 chunks)
     (1, 128, 64, 128),   # cfg 1, two tiles per row
