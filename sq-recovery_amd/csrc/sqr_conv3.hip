@@ -18,6 +18,7 @@
 // conflict-free, whatever the tap shift.  Halo / out-of-image pixels come back as zeros from the
 // buffer descriptor range check (voffset = 0x80000000).
 #include <stdint.h>
+#include <stdlib.h>
 #include "sqr_conv_dev.h"
 
 #ifndef SQR_EXP
@@ -110,17 +111,19 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
   stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(s1, s2, red, wm, wn, fr, fq, tid, stats_row0, stats_row1);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB>
+// IMGS > 1: a tile is IMGS whole images (TH x TW = H x W) with one halo window each, stacked in LDS
+// (small late-layer images: more pixels per weight tile fetched)
+template <int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
   constexpr int ROWB = 128, STAGES = 3;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int WWID = TW + 2, WR = (TH + 2) * WWID;          // halo window rows
+  constexpr int WWID = TW + 2, WRI = (TH + 2) * WWID, WR = IMGS * WRI;  // halo window rows
   constexpr int WROWS = (WR + 8 * NW - 1) / (8 * NW) * (8 * NW);
   constexpr int PB = BN / (8 * NW);                          // weight pieces per wave per step
   constexpr int WP = WROWS / (8 * NW);                       // window pieces per wave per chunk
-  static_assert(BM == TH * TW, "pixel tile");
+  static_assert(BM == IMGS * TH * TW, "pixel tile");
   static_assert(PB >= 1 && PB * 8 * NW == BN, "BN must be a multiple of 8 * waves");
   constexpr int WIN = WROWS * ROWB, TILE_B = BN * ROWB;
   constexpr int LDS = NWB * WIN + STAGES * TILE_B;
@@ -133,8 +136,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile_m = bid / a.ntn, tile_n = bid - (bid / a.ntn) * a.ntn;
-  const int img = tile_m / a.tiles_per_img;
-  const int trem = tile_m - img * a.tiles_per_img;
+  const int img = (tile_m / a.tiles_per_img) * IMGS;  // first image of the tile
+  const int trem = tile_m - (tile_m / a.tiles_per_img) * a.tiles_per_img;
   const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
   const int h0 = ty * TH, w0 = tx * TW, n0 = tile_n * BN;
 
@@ -146,10 +149,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   for (int i = 0; i < WP; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // window row
     const int ls = pslot ^ ((r >> 1) & 7);      // logical 16-B channel slot this lane fetches
-    const int wy = r / WWID, wx = r - wy * WWID;  // constant divisor
+    const int ii = r / WRI, rr = r - ii * WRI;     // image of the tile, row in its window
+    const int wy = rr / WWID, wx = rr - wy * WWID;  // constant divisors
     const int h = h0 - 1 + wy, w = w0 - 1 + wx;
     const bool ok = r < WR && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-    wvoff[i] = ok ? (uint32_t)((((img * a.H + h) * a.W + w) * a.Cin) * 2 + ls * 16) : kOOB;
+    wvoff[i] = ok ? (uint32_t)(((((img + ii) * a.H + h) * a.W + w) * a.Cin) * 2 + ls * 16) : kOOB;
   }
   uint32_t bvoff[PB];
 #pragma unroll
@@ -167,7 +171,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wm * WM + 16 * i + fr;
-    qbase[i] = (m / TW) * WWID + (m % TW);
+    const int ii = m / (TH * TW), mm = m - ii * (TH * TW);
+    qbase[i] = ii * WRI + (mm / TW) * WWID + (mm % TW);
   }
   int poff[TN];
 #pragma unroll
@@ -276,7 +281,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wm * WM + 16 * i + fr;
-    const size_t pix = ((size_t)img * a.H + h0 + m / TW) * a.W + w0 + (m % TW);
+    const int ii = m / (TH * TW), mm = m - ii * (TH * TW);
+    const size_t pix = ((size_t)(img + ii) * a.H + h0 + mm / TW) * a.W + w0 + (mm % TW);
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       *(u32x2*)(out + pix * a.Nout + n0 + wn * WN + 16 * j + 4 * fq) = u32x2{pk[j][i][0], pk[j][i][1]};
@@ -723,7 +729,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
 
 namespace {
 struct D3Cfg {
-  int id, BM, BN, threads, TW, TH, nwb;
+  int id, BM, BN, threads, TW, TH, nwb, imgs;
 };
 
 int g_direct = 1;  // 0 off, 1 on when the grid is big enough, 2 whenever the shape fits
@@ -740,18 +746,26 @@ int pow2_log(int x) {
 bool pick(int N, int H, int W, int Cin, int Nout, D3Cfg* out) {
   const int nch = Cin / 64;
   const D3Cfg cands[] = {
-      // id BM   BN  thr  TW TH nwb
-      {0, 256, 64, 256, 64, 4, 1},    // Nout 64, Cin 64 (layer1)
-      {1, 256, 128, 512, 32, 8, 2},   // W 32 (layer2)
-      {2, 128, 128, 512, 16, 8, 2},   // W 16 (layer3)
-      {3, 64, 128, 256, 8, 8, 2},     // W 8 (layer4)
+      // id BM   BN  thr  TW  TH nwb imgs
+      {0, 256, 64, 256, 64, 4, 1, 1},    // Nout 64, Cin 64 (layer1; the persistent kernel takes W 64)
+      {1, 256, 128, 512, 32, 8, 2, 1},   // W 32 (layer2)
+      {2, 128, 128, 512, 16, 8, 2, 1},   // W 16 (layer3)
+      {5, 128, 64, 256, 8, 8, 2, 2},     // 8 x 8, two images per tile (layer4: half the weight
+                                         // traffic of id 3, 28.4 vs 31.4 us fwd at B=64)
+      {3, 64, 128, 256, 8, 8, 2, 1},     // W 8 (layer4, odd batch)
+      {4, 256, 64, 256, 16, 16, 2, 1},   // W 16, whole image per tile (slower than id 2 on layer3)
+      {6, 256, 32, 256, 8, 8, 2, 4},     // 8 x 8, four images per tile
   };
+  int force = -1;
+  if (const char* e = getenv("SQR_D3_CFG")) force = atoi(e);  // experiments: force a configuration
   for (const D3Cfg& c : cands) {
+    if (force >= 0 && c.id != force) continue;
     if (c.id == 0 && !(Nout == 64 && nch == 1)) continue;
     if (c.id != 0 && Nout % c.BN) continue;
     if (W % c.TW || H % c.TH) continue;
+    if (c.imgs > 1 && (c.TH != H || c.TW != W || N % c.imgs)) continue;
     if (c.nwb == 1 && nch != 1) continue;
-    const long long tiles = (long long)N * (H / c.TH) * (W / c.TW) * (Nout / c.BN);
+    const long long tiles = (long long)(N / c.imgs) * (H / c.TH) * (W / c.TW) * (Nout / c.BN);
     if (tiles < 128 && g_direct < 2) continue;
     // measured (scratch/nt_tune.py, B=64): the direct kernel beats the implicit-GEMM one on every
     // ResNetSQ 3x3/s1 shape: layer2 25.0 vs 28.1 us, layer3 23.6 vs 29.7, layer4 29.1 vs 39.8
@@ -808,7 +822,7 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
   a.Nout = Nout;
   a.tiles_x = W / c.TW;
   a.tiles_per_img = (H / c.TH) * a.tiles_x;
-  a.ntm = N * a.tiles_per_img;
+  a.ntm = N / c.imgs * a.tiles_per_img;
   a.ntn = Nout / c.BN;
   a.flip = flip;
   a.xbytes = (uint32_t)xbytes;
@@ -820,7 +834,10 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
     case 0: hipLaunchKernelGGL((conv3_kernel<256, 64, 4, 1, 64, 4, 1>), grid, blk, 0, st, a); break;
     case 1: hipLaunchKernelGGL((conv3_kernel<256, 128, 4, 2, 32, 8, 2>), grid, blk, 0, st, a); break;
     case 2: hipLaunchKernelGGL((conv3_kernel<128, 128, 4, 2, 16, 8, 2>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3_kernel<64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((conv3_kernel<64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((conv3_kernel<256, 64, 4, 1, 16, 16, 2>), grid, blk, 0, st, a); break;
+    case 5: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3_kernel<256, 32, 4, 1, 8, 8, 2, 4>), grid, blk, 0, st, a); break;
   }
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_kernel");

@@ -126,7 +126,8 @@ DIRECT = [
     (2, 128, 32, 128),   # cfg 1 (TW 32 x TH 8, double-buffered window, 2 chunks)
     (1, 128, 64, 128),   # cfg 1, two tiles per row
     (2, 256, 16, 256),   # cfg 2 (TW 16 x TH 8)
-    (2, 512, 8, 512),    # cfg 3 (8 x 8, 8 chunks)
+    (2, 512, 8, 512),    # cfg 5 (two 8 x 8 images per tile, 8 chunks)
+    (3, 512, 8, 512),    # cfg 3 (odd batch: one image per tile)
     (2, 128, 16, 256),   # Cin != Nout
     (2, 64, 32, 128),    # fwd direct (cfg 1, one chunk); dgrad falls back
 ]
