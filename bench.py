@@ -32,7 +32,7 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-l
 PEAK_HBM_GBS = 8000.0
 
 # dominant kernel (largest share of step time in profiles/): the layer1 3x3 64->64 convs
-PROBE = ("wgrad", 64, 64, 3, 1)  # phase, C, H(=W), R, stride  (N = per-GPU batch)
+PROBE = ("fwd", 64, 64, 3, 1)  # phase, C, H(=W), R, stride  (N = per-GPU batch): layer-1 3x3 conv
 
 
 def conv_flops(N, C, H, K, R, stride):
@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--render", type=int, default=32, help="ImplicitLoss render size R")
-    ap.add_argument("--cpu-steps", type=int, default=2, help="timed CPU-baseline steps (0 = skip)")
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole train step in a HIP graph (1/0; default: on)")
@@ -199,7 +199,8 @@ def main():
     value = B * world * args.steps / dt
     flops = conv_flops(B, pc, ph, pc, pr, ps)
     achieved = flops / (kern_ms * 1e-3) / 1e12 if events else None
-    roof = {"bound": "mfma", "kernel": "conv_%s %dx%d %dx%d s%d (layer1, bf16)" % (PROBE[0], pc, pc, pr, pr, ps),
+    roof = {"bound": "mfma", "kernel": "conv_%s %dx%d %dx%d s%d (layer1 persistent direct conv, bf16)"
+                                       % (PROBE[0], pc, pc, pr, pr, ps),
             "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
             "kernel_ms": kern_ms, "launches": len(events), "traffic": None}

@@ -12,10 +12,10 @@ import json
 import os
 import sys
 
-# the probe kernel of bench.py (PROBE = wgrad, layer1 3x3 64->64): the direct weight-gradient kernel
-# instantiation used for 64-wide images (TW = 64) — only layer1 runs it
-DEFAULT_KERNEL = "conv3_wgrad_kernel<64, 2, 3>"
-PROBE_KEY = ["wgrad", 64, 64, 3, 1]
+# the probe kernel of bench.py (PROBE = fwd, layer1 3x3 64->64): the persistent direct conv, which
+# only layer1 runs (its forward and, with flipped taps, backward-data launches: same work and bytes)
+DEFAULT_KERNEL = "conv3p_kernel"
+PROBE_KEY = ["fwd", 64, 64, 3, 1]
 
 
 def per_dispatch(root, counter, kernel):
