@@ -13,9 +13,10 @@
 //   forward:       win = X,  Wt = w_krsc [K][3][3][C],  shift(r,s) = (r, s)
 //   backward-data: win = dY, Wt = w_crsk [C][3][3][K],  shift(r,s) = (2-r, 2-s)   (flip)
 //
-// LDS rows are 128 B (64 bf16 channels) with the same 16-B slot XOR swizzle as the NT kernel
-// (slot ^ ((row>>1)&7)): for any 16 consecutive window rows the ds_read_b128 fragment reads are
-// conflict-free, whatever the tap shift.  Halo / out-of-image pixels come back as zeros from the
+// LDS rows are 128 B (64 bf16 channels) with a 16-B slot XOR swizzle slot ^ (row & 6) (d3key):
+// for ANY 16 consecutive rows -- whatever the tap shift -- the ds_read_b128 fragment reads
+// (lanes fr = row offset 0..15, fq = slot) hit 16 distinct bank quads in every lane group.  (The
+// NT kernel's key (row>>1)&7 is conflict-free only for 16-aligned row groups: 2-way on 2/3 taps.)  Halo / out-of-image pixels come back as zeros from the
 // buffer descriptor range check (voffset = 0x80000000).
 #include <stdint.h>
 #include <stdlib.h>
@@ -24,11 +25,15 @@
 #ifndef SQR_EXP
 #define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop;
                    // conv3_kernel: 4 no per-tap wait/barrier, 8 no MFMA, 16 no fragment reads;
-                   // conv3p_kernel: 32 no output / statistics stores, 64 no tap loop)
+                   // conv3p_kernel: 128 no tap loop, 256 no output stores, 512 no row loads in
+                   // the tile loop, 1024 no fragment reads)
 #endif
 
 namespace sqr {
 namespace conv {
+
+// 16-B slot XOR key of a 128-B LDS row (see the header): shift-invariant conflict-free b128 reads
+__device__ __forceinline__ int d3key(int row) { return row & 6; }
 
 struct D3Args {
   const void* x;    // [N][H][W][Cin]
@@ -148,7 +153,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int i = 0; i < WP; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // window row
-    const int ls = pslot ^ ((r >> 1) & 7);      // logical 16-B channel slot this lane fetches
+    const int ls = pslot ^ d3key(r);      // logical 16-B channel slot this lane fetches
     const int ii = r / WRI, rr = r - ii * WRI;     // image of the tile, row in its window
     const int wy = rr / WWID, wx = rr - wy * WWID;  // constant divisors
     const int h = h0 - 1 + wy, w = w0 - 1 + wx;
@@ -159,7 +164,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int i = 0; i < PB; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // weight row = output channel n0 + r
-    const int ls = pslot ^ ((r >> 1) & 7);
+    const int ls = pslot ^ d3key(r);
     bvoff[i] = (uint32_t)(((n0 + r) * 9 * a.Cin) * 2 + ls * 16);
   }
   const __amdgpu_buffer_rsrc_t xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
@@ -178,7 +183,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int row = wn * WN + 16 * j + fr;
-    poff[j] = row * ROWB + ((fq ^ ((row >> 1) & 7)) << 4);  // slot fq; sub 1 = slot fq+4 = ^ 64 B
+    poff[j] = row * ROWB + ((fq ^ d3key(row)) << 4);  // slot fq; sub 1 = slot fq+4 = ^ 64 B
   }
 
   f32x4 acc[TN][TM];
@@ -220,7 +225,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
         int row = qbase[i] + toff;
         // keep the per-tap address math here: hoisted for all 9 unrolled taps it spills
         asm volatile("" : "+v"(row));
-        qoff[i] = row * ROWB + ((fq ^ ((row >> 1) & 7)) << 4);
+        qoff[i] = row * ROWB + ((fq ^ d3key(row)) << 4);
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
@@ -295,36 +300,55 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 
 
 // ============================================================================ layer-1 persistent
-// Cin = Nout = 64, W = 64 (ResNetSQ layer1, forward and backward-data): one workgroup per CU keeps
-// the whole 3x3 weight tensor (9 x 64 x 64 bf16 = 72 KiB) resident in LDS and walks 128-pixel
-// tiles (2 image rows of one image).  The halo window of its next tile streams in by LDS-DMA while
-// the current tile computes, and the current tile's output stores drain while the next one
-// computes (they are issued after the wait for the next window).  Two barriers per tile instead of
-// one per tap; no weight traffic after the first tile.
+// Cin = Nout = 64, W = 64 (ResNetSQ layer1, forward and backward-data).  One workgroup per band of
+// consecutive 2-row tiles of one image (B = 64: a quarter image = 8 tiles per workgroup):
+//  * the whole 3x3 weight tensor (9 x 64 x 64 bf16 = 72 KiB) is resident in LDS;
+//  * input rows live in an 8-slot LDS ring (slot = (row + 1) & 7; one image row + its 2 zero halo
+//    columns per slot): a tile reads 4 rows of which only 2 are new, and the new rows of the next
+//    TWO tiles stream in by LDS-DMA while the current tile computes, so every input row is fetched
+//    once per band and two tiles of loads are always in flight;
+//  * the output tile is staged in LDS and written with 16-B coalesced stores that drain while the
+//    next tile computes; BatchNorm partials accumulate in registers, one partial row per workgroup.
 struct D3PArgs {
   const void* x;   // [N][H][64][64]
   const void* w;   // [64][9][64]
   void* out;       // [N][H][64][64]
-  float* stats;    // nullable: BatchNorm partials [ntiles][2][64]
-  int H, ntiles, flip;
+  float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
+  int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
 };
+
+// s_waitcnt vmcnt(n) for the run-time n values the persistent kernel needs (wave-uniform)
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
 
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
   constexpr int WAVES_M = 2, WAVES_N = 2, WM = 64, WN = 32, TM = WM / 16, TN = WN / 16;
-  constexpr int WWID = TW + 2, WR = (TH + 2) * WWID;  // 264 halo-window rows
-  constexpr int WP = (WR + 8 * NW - 1) / (8 * NW);    // 9 window pieces per wave
-  constexpr int WIN = WP * 8 * NW * ROWB;             // 36 KiB per window buffer
-  constexpr int WPW = 9 * BN / (8 * NW);              // 18 weight pieces per wave
-  constexpr int WB = 9 * BN * ROWB;                   // 72 KiB: LDS row (tap, n)
-  constexpr int STG = TH * TW * BN * 2;                // 16 KiB staged output tile
-  constexpr int NST = STG / 16 / NT;                  // 16-B stores per thread per tile
-  static_assert(2 * WAVES_M * 16 * BN * 4 <= WIN, "statistics scratch fits a window buffer");
-  __shared__ __attribute__((aligned(1024))) char smem[WB + 2 * WIN + STG];  // 160 KiB
+  constexpr int SLOTR = 72;              // LDS rows per ring slot: 64 pixels + 2 halo, padded to 9 pieces
+  constexpr int PPR = SLOTR / 8;         // LDS-DMA pieces (8 rows = 1 KiB) per image row
+  constexpr int NSLOT = 8;
+  constexpr int RING = NSLOT * SLOTR * ROWB;  // 72 KiB
+  constexpr int WB = 9 * BN * ROWB;           // 72 KiB: LDS row (tap, n)
+  constexpr int WPW = 9 * BN / (8 * NW);      // 18 weight pieces per wave
+  constexpr int STG = TH * TW * BN * 2;       // 16 KiB staged output tile
+  constexpr int NST = STG / 16 / NT;          // 16-B stores per thread per tile
+  static_assert(WM == TW && TM * 16 == WM, "a wave's pixels are one image row");
+  static_assert(2 * WAVES_M * 16 * BN * 4 <= RING, "statistics scratch fits the ring");
+  __shared__ __attribute__((aligned(1024))) char smem[WB + RING + STG];  // 160 KiB
   char* const wl = smem;
-  char* const winb = smem + WB;
-  char* const stg = winb + 2 * WIN;
+  char* const ring = smem + WB;
+  char* const stg = ring + RING;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -333,7 +357,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr uint32_t kOOB = 0x80000000u;
   const __amdgpu_buffer_rsrc_t xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, a.wbytes, 0x00020000);
-  const int H = a.H, tiles_per_img = H / TH;
+  const int H = a.H, ntile = a.tpb;
+  const int img = blockIdx.x / a.bpi;
+  const int hb = (blockIdx.x - img * a.bpi) * ntile * TH;  // first output row of the band
 
   {  // resident weights: LDS row r = tap * 64 + n  <-  w[n][tap][0..63]
     uint32_t wv[WPW];
@@ -341,87 +367,103 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int i = 0; i < WPW; ++i) {
       const int r = (i * NW + wave) * 8 + prow;
       const int tap = r / BN, n = r - tap * BN;
-      wv[i] = (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4));
+      wv[i] = (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ d3key(r)) << 4));
     }
     dma_pieces<WPW, NW>(wsrd, wl, wv, 0, wave);
   }
-  auto issue_window = [&](int tile, char* dst) {
-    const int img = tile / tiles_per_img, h0 = (tile - img * tiles_per_img) * TH;
-    uint32_t vo[WP];
+  // LDS-DMA of input rows r0 .. r0+nrows-1 (row -1 / H: zero padding) into their ring slots; piece
+  // p (8 LDS rows of one image row) goes to wave p % 4.  Returns this wave's instruction count.
+  auto issue_rows = [&](int r0, int nrows) {
+    int cnt = 0;
 #pragma unroll
-    for (int i = 0; i < WP; ++i) {
-      const int r = (i * NW + wave) * 8 + prow;
-      const int wy = r / WWID, wx = r - wy * WWID;
-      const int h = h0 - 1 + wy, w = wx - 1;
-      const bool ok = r < WR && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)TW;
-      vo[i] = ok ? (uint32_t)((((img * H + h) * TW + w) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4)) : kOOB;
+    for (int i = 0; i < (4 * PPR + NW - 1) / NW; ++i) {
+      const int p = i * NW + wave;
+      if (p < nrows * PPR) {  // wave-uniform
+        const int j = p / PPR, part = p - j * PPR;
+        const int row = r0 + j;
+        const int lbase = ((row + 1) & (NSLOT - 1)) * SLOTR + part * 8;  // first LDS row of the piece
+        const int L = lbase + prow, w = part * 8 + prow - 1;
+        const bool ok = (unsigned)row < (unsigned)H && (unsigned)w < (unsigned)TW;
+        const uint32_t vo =
+            ok ? (uint32_t)((((img * H + row) * TW + w) * C) * 2 + ((pslot ^ d3key(L)) << 4)) : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xsrd, (__attribute__((address_space(3))) void*)(ring + lbase * ROWB),
+                                                 16, vo, 0, 0, 0);
+        ++cnt;
+      }
     }
-    dma_pieces<WP, NW>(xsrd, dst, vo, 0, wave);
+    return cnt;
   };
 
   const int fr = lane & 15, fq = lane >> 4;
-  int qbase[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wm * WM + 16 * i + fr;
-    qbase[i] = (m / TW) * WWID + (m % TW);
-  }
   int poff[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int row = wn * WN + 16 * j + fr;
-    poff[j] = row * ROWB + ((fq ^ ((row >> 1) & 7)) << 4);
+    poff[j] = row * ROWB + ((fq ^ d3key(row)) << 4);
   }
   const int flip = a.flip;
-
-  const int G = gridDim.x;
-  int tile = xcd_remap(blockIdx.x, G);  // an XCD's workgroups walk neighbouring tiles together
-  if (tile < a.ntiles) issue_window(tile, winb);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // BatchNorm partials accumulate over all of this workgroup's tiles: one partial row per workgroup
+  // BatchNorm partials accumulate over all of this workgroup's tiles
   float st1[TN][4], st2[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) st1[j][e] = st2[j][e] = 0.f;
-  // the previous tile's output leaves the staging area right after the next window's DMA is issued,
-  // so the wait for that window (vmcnt(NST)) never waits for output stores
-  auto store_staged = [&](int t) {
-    const int img = t / tiles_per_img, h0 = (t - img * tiles_per_img) * TH;
-    char* __restrict__ dst = (char*)a.out + ((size_t)img * H + h0) * TW * BN * 2;
+
+  auto store_staged = [&](int k) {
+    char* __restrict__ dst = (char*)a.out + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
 #pragma unroll
-    for (int k = 0; k < NST; ++k) {
-      const int c = k * NT + tid, row = c >> 3, slot = c & 7;
+    for (int q = 0; q < NST; ++q) {
+      const int c = q * NT + tid, row = c >> 3, slot = c & 7;
       const u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
+#if SQR_EXP & 256
+      if (v[0] == 0x12345678u && v[1] == 0x9abcdef0u) *(u32x4*)(dst + (size_t)c * 16) = v;
+#else
       *(u32x4*)(dst + (size_t)c * 16) = v;
+#endif
     }
   };
-  int buf = 0, prev = -1;
-  for (; tile < a.ntiles; tile += G) {
-    const char* win = winb + buf * WIN;
-    if (tile + G < a.ntiles) issue_window(tile + G, winb + (buf ^ 1) * WIN);
-    if (prev >= 0) store_staged(prev);
+
+  issue_rows(hb - 1, 4);                  // tile 0: rows hb-1 .. hb+2
+  if (ntile > 1) issue_rows(hb + 3, 2);   // tile 1's new rows
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int k = 0; k < ntile; ++k) {
+    // tile k+2's new rows go into the slots tile k-1 used (free since the last barrier)
+#if SQR_EXP & 512
+    const int pn = 0;
+#else
+    const int pn = k + 2 < ntile ? issue_rows(hb + 2 * (k + 2) + 1, 2) : 0;
+#endif
+    if (k >= 1) store_staged(k - 1);
     f32x4 acc[TN][TM];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // 18 (tap, k-half) steps, fragments software-pipelined one step ahead (one wave per SIMD:
-    // nothing else hides the LDS read latency)
+    // tap (r, c3) of output row hb+2k+wm reads input row hb+2k+wm+r-1 = ring slot (hb+2k+wm+r) & 7
+    const int rbase = hb + 2 * k + wm;
     auto load = [&](int s, bf16x8* pf, bf16x8* qf) {
       const int t = s >> 1, sub = s & 1;
       const int r = t / 3, c3 = t % 3;
-      const int toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
+      const int rr = flip ? 2 - r : r, cc = flip ? 2 - c3 : c3;
+      const int lrow0 = ((rbase + rr) & (NSLOT - 1)) * SLOTR + cc + fr;
       const char* wt = wl + t * BN * ROWB;
+#if SQR_EXP & 1024
+#pragma unroll
+      for (int j = 0; j < TN; ++j) pf[j] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)poff[j], (uint32_t)sub, 0u, 0u});
+#pragma unroll
+      for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)(lrow0 + i), 0u, 0u, 0u});
+      (void)wt;
+#else
 #pragma unroll
       for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(wt + (poff[j] ^ (sub << 6)));
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int row = qbase[i] + toff;
-        qf[i] = *(const bf16x8*)(win + ((row * ROWB + ((fq ^ ((row >> 1) & 7)) << 4)) ^ (sub << 6)));
+        const int L = lrow0 + 16 * i;
+        qf[i] = *(const bf16x8*)(ring + ((L * ROWB + ((fq ^ d3key(L)) << 4)) ^ (sub << 6)));
       }
+#endif
     };
     auto mma = [&](const bf16x8* pf, const bf16x8* qf) {
 #pragma unroll
@@ -429,20 +471,28 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
     };
-    bf16x8 pA[TN], qA[TM], pB[TN], qB[TM];
-    load(0, pA, qA);
-#if SQR_EXP & 64
-    if (a.ntiles < 0)
+    // 18 (tap, k-half) steps, fragments software-pipelined PD steps ahead (one wave per SIMD: its
+    // own reads in flight are all that hides the LDS latency)
+    constexpr int PD = 2;
+    bf16x8 pf[PD + 1][TN], qf[PD + 1][TM];
+#pragma unroll
+    for (int s = 0; s < PD; ++s) load(s, pf[s], qf[s]);
+#if SQR_EXP & 128
+    if (ntile < 0)
 #endif
 #pragma unroll
-    for (int s = 0; s < 18; s += 2) {
-      load(s + 1, pB, qB);
-      __builtin_amdgcn_sched_barrier(0);  // keep the reads a whole step ahead of their MFMAs
-      mma(pA, qA);
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 2 < 18) load(s + 2, pA, qA);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(pB, qB);
+    for (int s = 0; s < 18; ++s) {
+      if (s + PD < 18) load(s + PD, pf[(s + PD) % (PD + 1)], qf[(s + PD) % (PD + 1)]);
+      mma(pf[s % (PD + 1)], qf[s % (PD + 1)]);
+      // interleave: each fragment read (and its address VALU) rides in the gap of an MFMA, so the
+      // matrix pipe never idles while this wave issues the next step's reads
+#pragma unroll
+      for (int g = 0; g < TN + TM; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // up to 2 VALU
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, TN * TM - (TN + TM), 0);  // remaining MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
     uint32_t pk[TN][TM][2];
@@ -457,22 +507,10 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         pk[j][i][1] = __builtin_bit_cast(uint32_t, hi);
       }
     stats_accum<TM, TN>(pk, st1, st2);
-    // the next window has landed (only the NST younger output stores may still be in flight);
-    // after the barrier every wave is done with this window and with the staged previous tile
-    if (prev >= 0) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-#if SQR_EXP & 32
-    if (pk[0][0][0] == 0x12345678u) a.stats[tid] = 0.f;
-    buf ^= 1;
-    continue;
-#endif
-    // stage the 128 x 64 bf16 output tile (16 KiB, contiguous in NHWC); it is written back with
-    // 16-B per lane fully coalesced stores.  Row key (r ^ r>>3) & 7 on the 16-B slot: conflict-free
-    // reads, no 2-way write conflicts.
+    // tile k+1's rows (issued one iteration ago) have landed; younger in this wave's queue: the
+    // stores of tile k-2, the row loads of tile k+2 and the stores of tile k-1
+    wait_vm(pn + (k >= 1 ? NST : 0) + (k >= 2 ? NST : 0));
+    __builtin_amdgcn_s_barrier();  // ... for every wave; all waves are done with tile k's rows and the staging area
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = wm * WM + 16 * i + fr;
@@ -483,14 +521,12 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         *(u32x2*)(stg + m * ROWB + ((((n >> 3) ^ key) << 4) | ((n & 7) << 1))) = u32x2{pk[j][i][0], pk[j][i][1]};
       }
     }
-    __builtin_amdgcn_s_barrier();  // staged tile visible (LDS writes are waited by the barrier's lgkmcnt)
-    prev = tile;
-    buf ^= 1;
+    __builtin_amdgcn_s_barrier();  // staged tile visible
   }
-  if (prev >= 0) store_staged(prev);
+  if (ntile > 0) store_staged(ntile - 1);
   if (a.stats) {
     __syncthreads();
-    stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(st1, st2, (float*)winb, wm, wn, fr, fq, tid,
+    stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(st1, st2, (float*)ring, wm, wn, fr, fq, tid,
                                               a.stats + (size_t)blockIdx.x * 2 * BN,
                                               a.stats + ((size_t)blockIdx.x * 2 + 1) * BN);
   }
@@ -790,17 +826,23 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
       if (hipGetDevice(&dev) != hipSuccess) dev = 0;
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     }
+    // bands: the largest divisor of the per-image tile count giving about one workgroup per CU
+    const int tpi = H / 2;
+    int bpi = 1;
+    for (int d = 1; d <= tpi; ++d)
+      if (tpi % d == 0 && (long long)N * d <= ncu) bpi = d;
     D3PArgs p;
     p.x = x;
     p.w = w;
     p.out = out;
     p.stats = stats;
     p.H = H;
-    p.ntiles = N * (H / 2);
+    p.bpi = bpi;
+    p.tpb = tpi / bpi;
     p.flip = flip;
     p.xbytes = (uint32_t)xbytes;
     p.wbytes = (uint32_t)wbytes;
-    const int grid = p.ntiles < ncu ? p.ntiles : ncu;
+    const int grid = N * bpi;
     if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
     probe_begin(st);
     hipLaunchKernelGGL(conv3p_kernel, dim3(grid), dim3(256), 0, st, p);

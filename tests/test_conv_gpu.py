@@ -167,3 +167,37 @@ def test_conv3_direct(shape):
     assert _rel(res[2][0], res[0][0]) <= 8e-3
     assert _rel(res[2][1], res[0][1]) <= 8e-3
     assert _rel(res[2][3], res[0][3]) <= 2e-4
+
+
+@pytest.mark.parametrize("N", [64, 48, 128])
+def test_conv3_persistent_bands(N):
+    """The layer-1 persistent kernel at benchmark-sized batches (bands of 8 and 16 tiles per
+    workgroup, the 8-slot row ring wrapping several times) against the implicit-GEMM kernel on the
+    same bf16 inputs, plus its per-workgroup BatchNorm partials against the output itself."""
+    from sqr import conv as sc
+    from sqr._lib import lib
+    g = torch.Generator(device=DEV).manual_seed(N)
+    x = torch.randn(N, 64, 64, 64, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.randn(64, 64, 3, 3, device=DEV, generator=g) / 24.0
+    gy = torch.randn(N, 64, 64, 64, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    d = sc._desc(N, 64, 64, 64, 64, 3, 3, 1, 1, torch.bfloat16)
+    krsc, crsk = sc.pack_weight(w, d, True)
+    res = {}
+    old = lib().sqr_conv_set_direct(1)
+    try:
+        for mode in (1, 0):
+            lib().sqr_conv_set_direct(mode)
+            y, st = sc.conv2d_fwd(x, krsc, d, stats=True)
+            dx = sc.conv2d_bwd_data(gy, crsk, d)
+            torch.cuda.synchronize()
+            res[mode] = (y.float(), st.double().sum(0), dx.float(), st.shape[0])
+    finally:
+        lib().sqr_conv_set_direct(old)
+    y1, st1, dx1, rows1 = res[1]
+    y0, _, dx0, _ = res[0]
+    assert rows1 <= 256
+    assert _rel(y1, y0) <= 4e-3 and _rel(dx1, dx0) <= 4e-3
+    assert (y1 - y0).abs().max().item() <= 0.02 * y0.abs().max().item()
+    yd = y1.double()
+    assert _rel(st1[0], yd.sum((0, 2, 3))) <= 1e-5
+    assert _rel(st1[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
