@@ -32,6 +32,8 @@
 namespace sqr {
 namespace conv {
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
 // 16-B slot XOR key of a 128-B LDS row (see the header): shift-invariant conflict-free b128 reads
 __device__ __forceinline__ int d3key(int row) { return row & 6; }
 
@@ -334,7 +336,10 @@ __device__ __forceinline__ void wait_vm(int n) {
 
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
-  constexpr int WAVES_M = 2, WAVES_N = 2, WM = 64, WN = 32, TM = WM / 16, TN = WN / 16;
+  // 2 x 2 waves, each 64 pixels (one image row) x 32 channels = two 32x32 MFMA accumulators
+  // (v_mfma_f32_32x32x16_bf16: half the MFMA instructions of 16x16x32 for the same work, which
+  // leaves the single wave per SIMD issue slots for its LDS reads)
+  constexpr int WAVES_M = 2, WAVES_N = 2, WM = 64, WN = 32, TM = WM / 32;
   constexpr int SLOTR = 72;              // LDS rows per ring slot: 64 pixels + 2 halo, padded to 9 pieces
   constexpr int PPR = SLOTR / 8;         // LDS-DMA pieces (8 rows = 1 KiB) per image row
   constexpr int NSLOT = 8;
@@ -343,8 +348,8 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int WPW = 9 * BN / (8 * NW);      // 18 weight pieces per wave
   constexpr int STG = TH * TW * BN * 2;       // 16 KiB staged output tile
   constexpr int NST = STG / 16 / NT;          // 16-B stores per thread per tile
-  static_assert(WM == TW && TM * 16 == WM, "a wave's pixels are one image row");
-  static_assert(2 * WAVES_M * 16 * BN * 4 <= RING, "statistics scratch fits the ring");
+  static_assert(WM == TW && TM * 32 == WM && WN == 32, "a wave's pixels are one image row");
+  static_assert(2 * WAVES_M * 32 * BN * 4 <= RING, "statistics scratch fits the ring");
   __shared__ __attribute__((aligned(1024))) char smem[WB + RING + STG];  // 160 KiB
   char* const wl = smem;
   char* const ring = smem + WB;
@@ -367,7 +372,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int i = 0; i < WPW; ++i) {
       const int r = (i * NW + wave) * 8 + prow;
       const int tap = r / BN, n = r - tap * BN;
-      wv[i] = (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ d3key(r)) << 4));
+      wv[i] = (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4));
     }
     dma_pieces<WPW, NW>(wsrd, wl, wv, 0, wave);
   }
@@ -385,7 +390,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         const int L = lbase + prow, w = part * 8 + prow - 1;
         const bool ok = (unsigned)row < (unsigned)H && (unsigned)w < (unsigned)TW;
         const uint32_t vo =
-            ok ? (uint32_t)((((img * H + row) * TW + w) * C) * 2 + ((pslot ^ d3key(L)) << 4)) : kOOB;
+            ok ? (uint32_t)((((img * H + row) * TW + w) * C) * 2 + ((pslot ^ ((L >> 1) & 7)) << 4)) : kOOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xsrd, (__attribute__((address_space(3))) void*)(ring + lbase * ROWB),
                                                  16, vo, 0, 0, 0);
         ++cnt;
@@ -394,20 +399,15 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     return cnt;
   };
 
-  const int fr = lane & 15, fq = lane >> 4;
-  int poff[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int row = wn * WN + 16 * j + fr;
-    poff[j] = row * ROWB + ((fq ^ d3key(row)) << 4);
-  }
+  // 32x32x16 operand lanes: row r32 = lane & 31 (pixel / output channel), k half h = lane >> 5
+  const int r32 = lane & 31, h = lane >> 5;
+  const int prow32 = (wn * WN + r32) * ROWB;  // weight LDS row within a tap block (key (row>>1)&7)
+  const int pkey = ((wn * WN + r32) >> 1) & 7;
   const int flip = a.flip;
-  // BatchNorm partials accumulate over all of this workgroup's tiles
-  float st1[TN][4], st2[TN][4];
+  // BatchNorm partials (this lane: pixel column, 16 channels wn*32 + 8g + 4h + e) over all tiles
+  float st1[16], st2[16];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) st1[j][e] = st2[j][e] = 0.f;
+  for (int e = 0; e < 16; ++e) st1[e] = st2[e] = 0.f;
 
   auto store_staged = [&](int k) {
     char* __restrict__ dst = (char*)a.out + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
@@ -436,99 +436,110 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     const int pn = k + 2 < ntile ? issue_rows(hb + 2 * (k + 2) + 1, 2) : 0;
 #endif
     if (k >= 1) store_staged(k - 1);
-    f32x4 acc[TN][TM];
+    f32x16 acc[TM];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
     // tap (r, c3) of output row hb+2k+wm reads input row hb+2k+wm+r-1 = ring slot (hb+2k+wm+r) & 7
     const int rbase = hb + 2 * k + wm;
-    auto load = [&](int s, bf16x8* pf, bf16x8* qf) {
-      const int t = s >> 1, sub = s & 1;
+    // 36 (tap, 16-channel slice) steps; slice kk of a 128-B row = 16-B slots 2kk + h
+    auto load = [&](int s, bf16x8& pf, bf16x8* qf) {
+      const int t = s >> 2, kk = s & 3;
       const int r = t / 3, c3 = t % 3;
       const int rr = flip ? 2 - r : r, cc = flip ? 2 - c3 : c3;
-      const int lrow0 = ((rbase + rr) & (NSLOT - 1)) * SLOTR + cc + fr;
-      const char* wt = wl + t * BN * ROWB;
+      const int slot = 2 * kk + h;
+      const int lrow0 = ((rbase + rr) & (NSLOT - 1)) * SLOTR + cc + r32;
 #if SQR_EXP & 1024
-#pragma unroll
-      for (int j = 0; j < TN; ++j) pf[j] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)poff[j], (uint32_t)sub, 0u, 0u});
+      pf = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)(prow32 + slot), (uint32_t)t, 0u, 0u});
 #pragma unroll
       for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)(lrow0 + i), 0u, 0u, 0u});
-      (void)wt;
 #else
-#pragma unroll
-      for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(wt + (poff[j] ^ (sub << 6)));
+      pf = *(const bf16x8*)(wl + t * BN * ROWB + prow32 + ((slot ^ pkey) << 4));
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int L = lrow0 + 16 * i;
-        qf[i] = *(const bf16x8*)(ring + ((L * ROWB + ((fq ^ d3key(L)) << 4)) ^ (sub << 6)));
+        const int L = lrow0 + 32 * i;
+        qf[i] = *(const bf16x8*)(ring + L * ROWB + ((slot ^ ((L >> 1) & 7)) << 4));
       }
 #endif
     };
-    auto mma = [&](const bf16x8* pf, const bf16x8* qf) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
-    };
-    // 18 (tap, k-half) steps, fragments software-pipelined PD steps ahead (one wave per SIMD: its
-    // own reads in flight are all that hides the LDS latency)
-    constexpr int PD = 2;
-    bf16x8 pf[PD + 1][TN], qf[PD + 1][TM];
+    constexpr int NSTEP = 36, PD = 2;
+    bf16x8 pf[PD + 1], qf[PD + 1][TM];
 #pragma unroll
     for (int s = 0; s < PD; ++s) load(s, pf[s], qf[s]);
 #if SQR_EXP & 128
     if (ntile < 0)
 #endif
 #pragma unroll
-    for (int s = 0; s < 18; ++s) {
-      if (s + PD < 18) load(s + PD, pf[(s + PD) % (PD + 1)], qf[(s + PD) % (PD + 1)]);
-      mma(pf[s % (PD + 1)], qf[s % (PD + 1)]);
-      // interleave: each fragment read (and its address VALU) rides in the gap of an MFMA, so the
-      // matrix pipe never idles while this wave issues the next step's reads
+    for (int s = 0; s < NSTEP; ++s) {
+      if (s + PD < NSTEP) load(s + PD, pf[(s + PD) % (PD + 1)], qf[(s + PD) % (PD + 1)]);
 #pragma unroll
-      for (int g = 0; g < TN + TM; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // up to 2 VALU
+      for (int i = 0; i < TM; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[s % (PD + 1)], qf[s % (PD + 1)][i], acc[i], 0, 0, 0);
+#pragma unroll
+      for (int g = 0; g < 1 + TM; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // a fragment read
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // its address VALU
+        if (g < TM) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // an MFMA
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, TN * TM - (TN + TM), 0);  // remaining MFMAs
       __builtin_amdgcn_sched_barrier(0);
     }
-    uint32_t pk[TN][TM][2];
+    // lane holds D[n = wn*32 + 8g + 4h + e][pixel wm*64 + 32i + r32], g = reg >> 2, e = reg & 3
+    uint32_t pk[TM][4][2];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
+      for (int g = 0; g < 4; ++g) {
         typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        const bf16x2 lo = {(bf16)acc[j][i][0], (bf16)acc[j][i][1]};
-        const bf16x2 hi = {(bf16)acc[j][i][2], (bf16)acc[j][i][3]};
-        pk[j][i][0] = __builtin_bit_cast(uint32_t, lo);
-        pk[j][i][1] = __builtin_bit_cast(uint32_t, hi);
+        const bf16x2 lo = {(bf16)acc[i][4 * g], (bf16)acc[i][4 * g + 1]};
+        const bf16x2 hi = {(bf16)acc[i][4 * g + 2], (bf16)acc[i][4 * g + 3]};
+        pk[i][g][0] = __builtin_bit_cast(uint32_t, lo);
+        pk[i][g][1] = __builtin_bit_cast(uint32_t, hi);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float v0 = __uint_as_float(pk[i][g][q] << 16), v1 = __uint_as_float(pk[i][g][q] & 0xffff0000u);
+          st1[4 * g + 2 * q] += v0;
+          st2[4 * g + 2 * q] = fmaf(v0, v0, st2[4 * g + 2 * q]);
+          st1[4 * g + 2 * q + 1] += v1;
+          st2[4 * g + 2 * q + 1] = fmaf(v1, v1, st2[4 * g + 2 * q + 1]);
+        }
       }
-    stats_accum<TM, TN>(pk, st1, st2);
     // tile k+1's rows (issued one iteration ago) have landed; younger in this wave's queue: the
     // stores of tile k-2, the row loads of tile k+2 and the stores of tile k-1
     wait_vm(pn + (k >= 1 ? NST : 0) + (k >= 2 ? NST : 0));
     __builtin_amdgcn_s_barrier();  // ... for every wave; all waves are done with tile k's rows and the staging area
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int m = wm * WM + 16 * i + fr;
+      const int m = wm * WM + 32 * i + r32;
       const int key = (m ^ (m >> 3)) & 7;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = wn * WN + 16 * j + 4 * fq;
-        *(u32x2*)(stg + m * ROWB + ((((n >> 3) ^ key) << 4) | ((n & 7) << 1))) = u32x2{pk[j][i][0], pk[j][i][1]};
+      for (int g = 0; g < 4; ++g) {
+        const int n = wn * WN + 8 * g + 4 * h;
+        *(u32x2*)(stg + m * ROWB + ((((n >> 3) ^ key) << 4) | ((n & 7) << 1))) = u32x2{pk[i][g][0], pk[i][g][1]};
       }
     }
     __builtin_amdgcn_s_barrier();  // staged tile visible
   }
   if (ntile > 0) store_staged(ntile - 1);
-  if (a.stats) {
+  if (a.stats) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
     __syncthreads();
-    stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(st1, st2, (float*)ring, wm, wn, fr, fq, tid,
-                                              a.stats + (size_t)blockIdx.x * 2 * BN,
-                                              a.stats + ((size_t)blockIdx.x * 2 + 1) * BN);
+    float* red = (float*)ring;
+    float* r1 = red + (wm * 32 + r32) * BN + wn * WN + 4 * h;
+    float* r2 = r1 + 64 * BN;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      *(f32x4*)(r1 + 8 * g) = f32x4{st1[4 * g], st1[4 * g + 1], st1[4 * g + 2], st1[4 * g + 3]};
+      *(f32x4*)(r2 + 8 * g) = f32x4{st2[4 * g], st2[4 * g + 1], st2[4 * g + 2], st2[4 * g + 3]};
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int q = tid / BN, col = tid - q * BN;
+      const float* src = red + q * 64 * BN + col;
+      float sum = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < 64; ++r) sum += src[r * BN];
+      a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = sum;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
