@@ -32,6 +32,9 @@ PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-l
 PEAK_HBM_GBS = 8000.0
 
 # dominant kernel (largest share of step time in profiles/): the layer1 3x3 64->64 convs
+CONV_GFLOP_PER_IMG = 13.49  # ResNetSQ fwd + dgrad + wgrad per 256x256 image
+LOSS_TRANSC_PER_VOXEL = 21  # ImplicitLoss fwd (~13) + bwd (~8) transcendentals per voxel (§8(d))
+PEAK_TRANSC_TPS = 9.8       # 256 CU x 16 transcendentals/clk x 2.4 GHz (§8(d), datasheet-derived)
 PROBE = ("fwd", 64, 64, 3, 1)  # phase, C, H(=W), R, stride  (N = per-GPU batch): layer-1 3x3 conv
 
 
@@ -58,6 +61,29 @@ def cpu_baseline(images_cpu, state_dict, R, steps):
     return images_cpu.shape[0] * steps / dt, dt
 
 
+def time_loss_call(crit, images, B, dev, reps=20):
+    """GPU time of one fused ImplicitLoss call (forward + analytic gradient) at the bench shapes:
+    captured once in a HIP graph and replayed, so host launch gaps do not count."""
+    pred = (torch.rand(B, 12, device=dev) * 0.5 + 0.25).requires_grad_(True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        crit(images, pred)  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        crit(images, pred)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(path):
@@ -69,7 +95,7 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--render", type=int, default=32, help="ImplicitLoss render size R")
@@ -204,6 +230,18 @@ def main():
             "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
             "kernel_ms": kern_ms, "launches": len(events), "traffic": None}
+    # secondary rooflines: the whole step's conv work against the MFMA peak, and the
+    # fused loss call against the transcendental rate (per voxel ~21 exp2/log2/rcp, fwd + bwd)
+    loss_ms = time_loss_call(crit, images, B, dev) if rank == 0 else None
+    extra = {"conv_whole_step": {"gflop_per_image": CONV_GFLOP_PER_IMG,
+                                 "achieved": value * CONV_GFLOP_PER_IMG / 1e3, "peak": PEAK_BF16_TFLOPS,
+                                 "unit": "TFLOP/s",
+                                 "frac": value * CONV_GFLOP_PER_IMG / 1e3 / PEAK_BF16_TFLOPS}}
+    if loss_ms:
+        tps = B * R ** 3 * LOSS_TRANSC_PER_VOXEL / (loss_ms * 1e-3) / 1e12
+        extra["implicit_loss"] = {"call_ms_graph": loss_ms, "achieved": tps, "peak": PEAK_TRANSC_TPS,
+                                  "unit": "T transcendentals/s", "frac": tps / PEAK_TRANSC_TPS,
+                                  "hbm_bytes_per_image": R * R * 4 + 96}
     tr = load_traffic()
     if tr and tr.get("kernel_key") == list(PROBE):
         roof["traffic"] = tr.get("hbm_bytes_per_launch")
@@ -218,7 +256,7 @@ def main():
                       "parallelism": "dp%d" % world},
            "mean_loss": mean_loss, "hip_graph": use_graph,
            "dp": ("graph-captured RCCL all-reduce" if gdp is not None else ("DDP" if world > 1 else None)),
-           "roofline": roof}
+           "roofline": roof, "roofline_extra": extra}
 
     if rank == 0 and world == 1 and args.cpu_steps > 0:
         imgs_cpu = images.detach().cpu()
