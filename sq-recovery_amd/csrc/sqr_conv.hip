@@ -554,39 +554,38 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 
 // dw_kcrs[k][c][r][s] = sum_z slab[z][k][(r*S+s)*Ci + c]   (c < C real channels)
 // im2col mode: column index = (r*S+s)*C + c directly (Ci = padded K of the col matrix).
-// Block = 16 column-quads x 16 split-lanes: lane z0 sums splits z0, z0+16, ... (16-B coalesced
-// reads), then the 16 partial sums are added in a fixed order through LDS -> deterministic.
+// Block = QB column-quads x ZL split-lanes (QB * ZL = 256; ZL = the largest power of two <=
+// min(16, splits), so no lane idles when there are few splits): lane z0 sums splits z0, z0+ZL, ...
+// with 8 independent 16-B loads in flight (the pass is HBM/MALL-bound and needs the bytes in
+// flight), then the ZL partial sums are added in a fixed order through LDS -> deterministic.
 // The permuted writes to torch's KCRS layout are 4-B scatters (the output is small).
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int K,
-                                                           int Ng, int C, int R, int S, int Ci, int im2col,
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int zl_log2,
+                                                           int K, int Ng, int C, int R, int S, int Ci, int im2col,
                                                            float* __restrict__ dw) {
-  __shared__ f32x4 part[16][17];
+  __shared__ f32x4 part[256];
+  const int ZL = 1 << zl_log2, QB = 256 >> zl_log2;
   const int nq = Ng >> 2;
-  const int ql = threadIdx.x & 15, zl = threadIdx.x >> 4;
-  const int qidx = blockIdx.x * 16 + ql;  // over K * Ng/4
+  const int ql = threadIdx.x & (QB - 1), zl = threadIdx.x >> (8 - zl_log2);
+  const int qidx = blockIdx.x * QB + ql;  // over K * Ng/4
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const size_t stride = (size_t)K * Ng;
   if (qidx < K * nq) {
     const int k = qidx / nq, col0 = (qidx - k * nq) * 4;
     const float* src = slab + (size_t)k * Ng + col0;
     int z = zl;
-    // 4 independent loads in flight per step (the split count is a runtime value)
-    for (; z + 48 < splits; z += 64) {
-      const f32x4 a0 = *(const f32x4*)(src + (size_t)z * stride);
-      const f32x4 a1 = *(const f32x4*)(src + (size_t)(z + 16) * stride);
-      const f32x4 a2 = *(const f32x4*)(src + (size_t)(z + 32) * stride);
-      const f32x4 a3 = *(const f32x4*)(src + (size_t)(z + 48) * stride);
-      acc += a0;
-      acc += a1;
-      acc += a2;
-      acc += a3;
+    for (; z + 7 * ZL < splits; z += 8 * ZL) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(src + (size_t)(z + u * ZL) * stride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
     }
-    for (; z < splits; z += 16) acc += *(const f32x4*)(src + (size_t)z * stride);
+    for (; z < splits; z += ZL) acc += *(const f32x4*)(src + (size_t)z * stride);
   }
-  part[zl][ql] = acc;
+  part[threadIdx.x] = acc;  // [zl][ql]
   __syncthreads();
   if (zl != 0 || qidx >= K * nq) return;
-  for (int z = 1; z < 16; ++z) acc += part[z][ql];
+  for (int z = 1; z < ZL; ++z) acc += part[z * QB + ql];
   const int k = qidx / nq, col0 = (qidx - k * nq) * 4;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -602,6 +601,51 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     }
     dw[((size_t)k * C + c) * R * S + tap] = acc[e];
   }
+}
+
+// Same sum for the (tap, c) column layout (Ci == C), organised so that the permuted KCRS output
+// is written with coalesced stores: a block owns output channel k and 64 input channels c0..c0+63,
+// i.e. the contiguous run dw[k][c0..c0+63][0..RS-1].  Thread (lane, tap, quad) sums the splits
+// lane, lane+ZL, ... of slab[.][k][tap*C + c0 + 4*quad ..+3] (8 loads in flight); the ZL partials
+// are added in a fixed order and the block's 64*RS results leave through an LDS transpose.
+// Used when the split count is small and the output large (layers 3-4: 4.7 MB, 4 splits), where
+// the 4-B scatters of wgrad_reduce_kernel dominated.
+__global__ void __launch_bounds__(256) wgrad_reduce_tc_kernel(const float* __restrict__ slab, int splits,
+                                                              int zl_log2, int K, int C, int RS,
+                                                              float* __restrict__ dw) {
+  __shared__ f32x4 part[256];
+  __shared__ float outb[64 * 16];
+  const int ZL = 1 << zl_log2;
+  const int nq = RS * 16;  // (tap, quad) pairs of the block
+  const int cgroups = C >> 6;
+  const int k = blockIdx.x / cgroups, c0 = (blockIdx.x - k * cgroups) * 64;
+  const int t = threadIdx.x;
+  const int zl = t / nq, pq = t - zl * nq;  // lanes beyond ZL * nq idle
+  const int tap = pq >> 4, q = pq & 15;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const size_t stride = (size_t)K * RS * C;
+  if (zl < ZL) {
+    const float* src = slab + ((size_t)k * RS + tap) * C + c0 + 4 * q;
+    int z = zl;
+    for (; z + 7 * ZL < splits; z += 8 * ZL) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const f32x4*)(src + (size_t)(z + u * ZL) * stride);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; z < splits; z += ZL) acc += *(const f32x4*)(src + (size_t)z * stride);
+    part[t] = acc;
+  }
+  __syncthreads();
+  if (t < nq) {
+    for (int z = 1; z < ZL; ++z) acc += part[z * nq + t];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) outb[(4 * q + e) * RS + tap] = acc[e];
+  }
+  __syncthreads();
+  float* __restrict__ dst = dw + ((size_t)k * C + c0) * RS;
+  for (int i = t; i < 64 * RS; i += 256) dst[i] = outb[i];
 }
 
 // ============================================================================ helpers
@@ -936,6 +980,31 @@ int launch_tn(TNArgs a, const TNPlan& p, hipStream_t st) {
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// split-lanes: the largest power of two <= min(cap, splits)
+int reduce_zl_log2(int splits, int cap = 16) {
+  int l = 0;
+  while ((2 << l) <= cap && (2 << l) <= splits) ++l;
+  return l;
+}
+
+// fixed-order split-K sum of the weight-gradient slabs into torch's [K][C][R][S]
+int launch_wgrad_reduce(const float* slab, int splits, int K, int Ng, int C, int R, int S, int Ci, int im2col,
+                        float* dw, hipStream_t st) {
+  const int RS = R * S;
+  if (!im2col && Ci == C && C % 64 == 0 && RS <= 16 && splits <= 16) {
+    const int zlg = reduce_zl_log2(splits, 256 / (RS * 16));
+    hipLaunchKernelGGL(wgrad_reduce_tc_kernel, dim3(K * (C / 64)), dim3(256), 0, st, slab, splits, zlg, K, C, RS, dw);
+    SQR_HIP_LAUNCH_CHECK("wgrad_reduce_tc_kernel");
+    return 0;
+  }
+  const int total = K * (Ng / 4);
+  const int zlg = reduce_zl_log2(splits);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + (256 >> zlg) - 1) / (256 >> zlg)), dim3(256), 0, st, slab,
+                     splits, zlg, K, Ng, C, R, S, Ci, im2col, dw);
+  SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
+  return 0;
+}
+
 }  // namespace
 
 // ============================================================================ C ABI
@@ -1157,10 +1226,8 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
     const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
     rc = conv3w_launch(x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
     if (rc == 0) {
-      const int total = d->K * (Ng / 4);
-      hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, st, (const float*)ws, splits,
-                         d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs);
-      SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
+      rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st);
+      if (rc) return rc;
       return 0;
     }
     if (rc != 1) return rc;
@@ -1178,10 +1245,8 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   const TNPlan p = plan_tn(d->K, Ng, sh.M, sh.ES);
   rc = d->dtype == SQR_DTYPE_BF16 ? launch_tn<bf16>(a, p, st) : launch_tn<float>(a, p, st);
   if (rc) return rc;
-  const int total = d->K * (Ng / 4);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 15) / 16), dim3(256), 0, st, (const float*)ws, p.splits,
-                     d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C, (int)sh.im2col, dw_kcrs);
-  SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
+  return launch_wgrad_reduce((const float*)ws, p.splits, d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C,
+                             (int)sh.im2col, dw_kcrs, st);
   return 0;
 }
 
