@@ -104,6 +104,11 @@ def main():
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole train step in a HIP graph (1/0; default: on)")
     args = ap.parse_args()
+    # stdout carries exactly ONE line (the JSON result): native libraries that print to fd 1 (RCCL's
+    # version banner at communicator init) are redirected to stderr; the JSON goes to a saved fd
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     from sqr import dist
     rank, world, dev = dist.init("nccl")
@@ -169,13 +174,26 @@ def main():
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(graph):
-            static_loss = body()
+        try:
+            with torch.cuda.graph(graph):
+                static_loss = body()
+        except Exception as e:  # N > 1 only: keep the run alive on eager DDP (reported in "dp")
+            if gdp is None:
+                raise
+            print("bench: capturing the data-parallel step failed (%s: %s); eager DDP instead"
+                  % (type(e).__name__, e), file=sys.stderr)
+            torch.cuda.synchronize()
+            gdp.close(opt)
+            gdp = None
+            model = dist.wrap(net, dev)
+            use_graph = False
+            graph = None
 
-        def graph_step():
-            graph.replay()
-            return static_loss
-        step = graph_step
+        if use_graph:
+            def graph_step():
+                graph.replay()
+                return static_loss
+            step = graph_step
 
     def barrier():
         dist.barrier()
@@ -266,7 +284,7 @@ def main():
                                          "fp32 + reference-style f64 ImplicitLoss(R=%d), Adam; %.1f s"
                                          % (args.cpu_steps, B, R, secs)}
     if rank == 0:
-        print(json.dumps(out))
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     dist.finish()
 
 
