@@ -103,18 +103,28 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
         for (int i = 0; i < 8; ++i) g[u][i] = (mb >> i) & 1 ? g[u][i] : 0.f;
       }
     }
+    // the U pixels of this step in f32 (8 terms), the running sums in f64: one f64 add per
+    // channel and statistic per step instead of per element (the f64 VALU work was the bound)
+    float fa[8], fb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = fb[i] = 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if (MODE == 0) {
-          sa[i] += (double)xv[u][i];
-          sb[i] += (double)xv[u][i] * (double)xv[u][i];
+          fa[i] += xv[u][i];
+          fb[i] = fmaf(xv[u][i], xv[u][i], fb[i]);
         } else {
-          sa[i] += (double)g[u][i];
-          sb[i] += (double)g[u][i] * (double)(xv[u][i] - mu[i]);
+          fa[i] += g[u][i];
+          fb[i] = fmaf(g[u][i], xv[u][i] - mu[i], fb[i]);
         }
       }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sa[i] += (double)fa[i];
+      sb[i] += (double)fb[i];
     }
   }
   double* dst = red + ((size_t)row * V + v) * 16;
