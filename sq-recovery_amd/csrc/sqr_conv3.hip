@@ -120,10 +120,12 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 
 // IMGS > 1: a tile is IMGS whole images (TH x TW = H x W) with one halo window each, stacked in LDS
 // (small late-layer images: more pixels per weight tile fetched)
-template <int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1>
+// PD: weight tiles prefetched ahead (ring of PD + 1 stages): the per-CU LDS-DMA delivery is
+// latency x bytes-in-flight bound, so deeper rings buy throughput where LDS allows
+template <int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
-  constexpr int ROWB = 128, STAGES = 3;
+  constexpr int ROWB = 128, STAGES = PD + 1;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int WWID = TW + 2, WRI = (TH + 2) * WWID, WR = IMGS * WRI;  // halo window rows
@@ -196,11 +198,27 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 
   const int nch = a.Cin >> 6;
   const int flip = a.flip;
-  auto b_soff = [&](int cc, int t) { return __builtin_amdgcn_readfirstlane((t * a.Cin + cc * 64) * 2); };
+  const int nsteps = nch * 9;
+  static_assert(NWB == 2 || PD == 2, "single-window configurations keep the 3-stage ring");
+  static_assert(PB * (PD - 1) + WP <= 63, "vmcnt range");
+  static_assert(PD >= 2 && PD <= 8, "the next window must be older than the tile retired at tap 8");
+  // weight tile of global step q = 9 * chunk + tap (clamped: the dummy reloads past the end keep
+  // every wave's count of loads in flight uniform, and land in slots nobody reads again)
+  auto issue_w = [&](int q) {
+    q = q < nsteps ? q : nsteps - 1;
+    const int cq = q / 9, tq = q - cq * 9;
+    dma_pieces<PB, NW>(wsrd, bring + ((q % STAGES) * TILE_B), bvoff,
+                       __builtin_amdgcn_readfirstlane((tq * a.Cin + cq * 64) * 2), wave);
+  };
   dma_pieces<WP, NW>(xsrd, smem, wvoff, 0, wave);
-  dma_pieces<PB, NW>(wsrd, bring, bvoff, b_soff(0, 0), wave);
-  dma_pieces<PB, NW>(wsrd, bring + TILE_B, bvoff, b_soff(0, 1), wave);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+#pragma unroll
+  for (int q = 0; q < PD; ++q) issue_w(q);
+  // window 0 and weight tile 0 landed; tiles 1 .. PD-1 stay in flight
+  if constexpr (PD == 2) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+  }
   __builtin_amdgcn_s_barrier();
 
   for (int cc = 0; cc < nch; ++cc) {
@@ -208,19 +226,28 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     const char* win = smem + (NWB == 2 ? (cc & 1) * WIN : 0);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      // prefetch the weight tile two steps ahead: (cc, t+2) or (cc+1, t-7); ring stage = step % 3
-      const bool more = t < 7 || next;
-      if (t < 7) {
-        dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff, b_soff(cc, t + 2), wave);
-      } else if (next) {
-        dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff, b_soff(cc + 1, t - 7), wave);
+      const int step = cc * 9 + t;
+      if constexpr (PD == 2) {
+        // (the original 3-stage schedule: no loads past the end)
+        if (t < 7) {
+          dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff,
+                             __builtin_amdgcn_readfirstlane(((t + 2) * a.Cin + cc * 64) * 2), wave);
+        } else if (next) {
+          dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff,
+                             __builtin_amdgcn_readfirstlane(((t - 7) * a.Cin + (cc + 1) * 64) * 2), wave);
+        }
+        if (NWB == 2 && t == 0 && next)
+          dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff, __builtin_amdgcn_readfirstlane((cc + 1) * 128),
+                             wave);
+      } else {
+        issue_w(step + PD);
+        if (t == 0)  // next chunk's window (the last chunk reloads its own into the idle buffer)
+          dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff,
+                             __builtin_amdgcn_readfirstlane((next ? cc + 1 : cc) * 128), wave);
       }
-      if (NWB == 2 && t == 0 && next)
-        dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff, __builtin_amdgcn_readfirstlane((cc + 1) * 128),
-                           wave);
       const int r = t / 3, c3 = t % 3;
       const int toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
-      const char* bst = bring + (t % 3) * TILE_B;
+      const char* bst = bring + (PD == 2 ? (t % 3) : (step % STAGES)) * TILE_B;
       int qoff[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -255,21 +282,32 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
 #endif
       }
-#if SQR_EXP & 4
-      if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      continue;
-#endif
-      // retire the weight tile of the next step (and at tap 8 the next window, which is older);
-      // at taps 0-1 the next chunk's window is younger than it and stays in flight
-      if (!more) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if (NWB == 2 && t <= 1 && next) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB + WP) : "memory");
+      if constexpr (PD == 2) {
+        const bool more = t < 7 || next;
+        // retire the weight tile of the next step (and at tap 8 the next window, which is older);
+        // at taps 0-1 the next chunk's window is younger than it and stays in flight
+        if (!more) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (NWB == 2 && t <= 1 && next) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB + WP) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+        }
       } else {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+        // retire weight tile step+1 (issued at step+1-PD): younger are tiles step+2 .. step+PD and,
+        // for t <= PD-1, this chunk's window load (issued at t = 0 after that step's tile load)
+        if (t <= PD - 1) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1) + WP) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+        }
       }
       __builtin_amdgcn_s_barrier();
     }
+  }
+  if constexpr (PD != 2) {  // drain the dummy loads before the epilogue reuses the LDS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 
   // ---- epilogue: lane holds out[pixel m][n..n+3]; convert once, store, then BN partials
@@ -795,10 +833,15 @@ bool pick(int N, int H, int W, int Cin, int Nout, D3Cfg* out) {
   const D3Cfg cands[] = {
       // id BM   BN  thr  TW  TH nwb imgs
       {0, 256, 64, 256, 64, 4, 1, 1},    // Nout 64, Cin 64 (layer1; the persistent kernel takes W 64)
-      {1, 256, 128, 512, 32, 8, 2, 1},   // W 32 (layer2)
-      {2, 128, 128, 512, 16, 8, 2, 1},   // W 16 (layer3)
-      {5, 128, 64, 256, 8, 8, 2, 2},     // 8 x 8, two images per tile (layer4: half the weight
-                                         // traffic of id 3, 28.4 vs 31.4 us fwd at B=64)
+      // deeper weight rings first (bitwise the same results; B=64 fwd: layer2 24.8 vs 25.7 us,
+      // layer3 23.5 vs 23.9, layer4 27.1 vs 28.4 -- scratch/d3_cfg.py)
+      {7, 256, 128, 512, 32, 8, 2, 1},   // W 32 (layer2), 4-stage weight ring
+      {8, 128, 128, 512, 16, 8, 2, 1},   // W 16 (layer3), 6-stage ring
+      {10, 128, 64, 256, 8, 8, 2, 2},    // 8 x 8, two images per tile (layer4), 9-stage ring
+      {1, 256, 128, 512, 32, 8, 2, 1},   // W 32, 3-stage ring
+      {2, 128, 128, 512, 16, 8, 2, 1},   // W 16, 3-stage ring
+      {5, 128, 64, 256, 8, 8, 2, 2},     // 8 x 8, two images per tile (half the weight traffic of id 3)
+      {9, 128, 64, 256, 8, 8, 2, 2},     // id 5 with a 6-stage ring
       {3, 64, 128, 256, 8, 8, 2, 1},     // W 8 (layer4, odd batch)
       {4, 256, 64, 256, 16, 16, 2, 1},   // W 16, whole image per tile (slower than id 2 on layer3)
       {6, 256, 32, 256, 8, 8, 2, 4},     // 8 x 8, four images per tile
@@ -890,7 +933,11 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
     case 3: hipLaunchKernelGGL((conv3_kernel<64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
     case 4: hipLaunchKernelGGL((conv3_kernel<256, 64, 4, 1, 16, 16, 2>), grid, blk, 0, st, a); break;
     case 5: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3_kernel<256, 32, 4, 1, 8, 8, 2, 4>), grid, blk, 0, st, a); break;
+    case 6: hipLaunchKernelGGL((conv3_kernel<256, 32, 4, 1, 8, 8, 2, 4>), grid, blk, 0, st, a); break;
+    case 7: hipLaunchKernelGGL((conv3_kernel<256, 128, 4, 2, 32, 8, 2, 1, 3>), grid, blk, 0, st, a); break;
+    case 8: hipLaunchKernelGGL((conv3_kernel<128, 128, 4, 2, 16, 8, 2, 1, 5>), grid, blk, 0, st, a); break;
+    case 9: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2, 5>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2, 8>), grid, blk, 0, st, a); break;
   }
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_kernel");
