@@ -128,13 +128,15 @@ int sqr_conv2d_pack_weights(const sqr_pack_job* jobs, int njobs, void* stream);
 int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, void* workspace,
                    size_t workspace_bytes, void* stream);
 /* Forward that also emits BatchNorm batch-statistics partials of the (dtype-rounded) output:
- * stats[rows][2][K] f32 = per M-tile (sum, sum of squares) per output channel, *stats_rows = rows.
+ * stats[rows][2][K] f32 = (sum, sum of squares) per output channel over disjoint pixel sets (M tiles,
+ * or the per-workgroup bands of the persistent layer-1 kernel), *stats_rows = rows.
  * stats must hold sqr_conv2d_stats_floats(d) floats.  Feed them to sqr_bn_fwd_stats /
  * sqr_stem_fwd_stats so the BatchNorm that follows the conv never re-reads the activation. */
 size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
 /* Routing of bf16 3x3/stride-1/pad-1 forward and backward-data convs to the direct halo-window
- * kernel: 1 (default) when the shape tiles and the grid fills the chip, 2 whenever the shape
- * tiles, 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.
+ * kernels (C = K = 64, W = 64: the persistent resident-weight kernel; otherwise the tiled one):
+ * 1 (default) when the shape tiles and the grid fills the chip, 2 whenever the shape tiles,
+ * 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.
  * Process-wide; meant for A/B tests. */
 int sqr_conv_set_direct(int mode);
 int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
