@@ -1159,6 +1159,12 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
     rc = conv3_launch(dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, st);
     if (rc != 1) return rc;
   }
+  if (d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 2 && d->pad == 1 &&
+      d->H == 2 * sh.Ho && d->W == 2 * sh.Wo) {
+    const int off[4] = {0, d->C * d->K, 3 * d->C * d->K, 5 * d->C * d->K};  // classes of 1, 2, 2, 4 taps
+    rc = conv3s2_dgrad_launch(dy, w_crsk, off, dx, d->N, sh.Ho, sh.Wo, d->K, d->C, st);
+    if (rc != 1) return rc;
+  }
   // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+p-r)/st,(w+p-s)/st,k] W[k,c,r,s] over the divisible taps.
   // Output pixels split by parity (h%st, w%st); in class (ph,pw) only taps r = r0 + st*t contribute
   // and dY row = i + off_h - t: a stride-1 implicit GEMM over the class grid (Hc x Wc).

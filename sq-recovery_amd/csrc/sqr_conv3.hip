@@ -582,6 +582,170 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ============================================================================ stride-2 dgrad
+// Backward-data of a 3x3 / stride-2 / pad-1 conv (ResNetSQ's first conv of layers 2-3) as ONE
+// direct kernel.  dX pixel (2i+ph, 2j+pw) only receives the taps of its parity class:
+//   class (ph, pw) has taps t < Rc, u < Sc (Rc = 1 + ph, Sc = 1 + pw) reading dY[i + ph - t][j + pw - u]
+// (sqr_conv2d_bwd_data's classes; weights packed per class [C][Rc][Sc][K]).  A workgroup owns a
+// TH x TW block of dY positions of one image and BN output channels; the dY halo window
+// ((TH+1) x (TW+1) positions) of EVERY 64-channel chunk is staged once (all chunks resident), then
+// the four classes run one after the other — each a shifted-window GEMM over its 1/2/2/4 taps with
+// its own accumulators and epilogue — while the class/chunk/tap weight tiles stream through an
+// LDS-DMA ring.  Replaces the implicit GEMM whose per-class K (128-512) was too short to amortise
+// its pipeline (layer 2: 38 us at 0.25 of peak).
+struct D3S2Args {
+  const void* dy;  // [N][Ho][Wo][K]
+  const void* w;   // parity classes back to back, class cl = [C][Rc][Sc][K]
+  void* dx;        // [N][2Ho][2Wo][C]
+  int N, Ho, Wo, K, C;
+  int tiles_x, tiles_per_img, ntn;
+  int cls_off[4];  // elements
+  uint32_t dybytes, wbytes;
+};
+
+__host__ __device__ constexpr int s2_ntaps(int cl) { return (1 + (cl >> 1)) * (1 + (cl & 1)); }
+
+template <int TH, int TW, int BN, int WAVES_M, int WAVES_N, int NCH, int PD>
+__global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D3S2Args a) {
+  constexpr int NW = WAVES_M * WAVES_N, ROWB = 128, STAGES = PD + 1;
+  constexpr int BM = TH * TW, WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
+  constexpr int WWID = TW + 1, WR = (TH + 1) * WWID;
+  constexpr int WROWS = (WR + 8 * NW - 1) / (8 * NW) * (8 * NW);
+  constexpr int WP = WROWS / (8 * NW), PB = BN / (8 * NW);
+  constexpr int WIN = WROWS * ROWB, TILE_B = BN * ROWB;
+  constexpr int NSTEP = 9 * NCH;
+  static_assert(PB >= 1 && PB * 8 * NW == BN, "BN must be a multiple of 8 * waves");
+  static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0, "wave tile");
+  static_assert(PB * (PD - 1) <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) char smem[NCH * WIN + STAGES * TILE_B];
+  char* const bring = smem + NCH * WIN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_m = bid / a.ntn, tile_n = bid - tile_m * a.ntn;
+  const int img = tile_m / a.tiles_per_img, trem = tile_m - img * a.tiles_per_img;
+  const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
+  const int i0 = ty * TH, j0 = tx * TW, n0 = tile_n * BN;
+  constexpr uint32_t kOOB = 0x80000000u;
+  const int prow = lane >> 3, pslot = lane & 7;
+  const __amdgpu_buffer_rsrc_t dsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, a.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, a.wbytes, 0x00020000);
+
+  // dY windows of all chunks: window row r = (y, x) -> dY position (i0 + y, j0 + x)
+  {
+    uint32_t wvoff[WP];
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int r = (i * NW + wave) * 8 + prow;
+      const int y = r / WWID, x = r - y * WWID;
+      const int h = i0 + y, w = j0 + x;
+      const bool ok = r < WR && h < a.Ho && w < a.Wo;
+      wvoff[i] = ok ? (uint32_t)((((img * a.Ho + h) * a.Wo + w) * a.K) * 2 + ((pslot ^ d3key(r)) << 4)) : kOOB;
+    }
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc)
+      dma_pieces<WP, NW>(dsrd, smem + cc * WIN, wvoff, __builtin_amdgcn_readfirstlane(cc * 128), wave);
+  }
+  // weight tile of step q: class cl, chunk cc, tap tt -> rows c = n0 + row of class cl
+  int wrow[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) wrow[i] = n0 + (i * NW + wave) * 8 + prow;
+  auto issue_w = [&](int q) {
+    q = q < NSTEP ? q : NSTEP - 1;  // dummy reloads past the end keep the per-wave counts uniform
+    int cl = 0, rem = q;
+    while (rem >= s2_ntaps(cl) * NCH) {
+      rem -= s2_ntaps(cl) * NCH;
+      ++cl;
+    }
+    const int nt = s2_ntaps(cl), cc = rem / nt, tt = rem - cc * nt;
+    uint32_t vo[PB];
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int rr = (i * NW + wave) * 8 + prow;
+      vo[i] = (uint32_t)(((size_t)a.cls_off[cl] + ((size_t)wrow[i] * nt + tt) * a.K + cc * 64) * 2 +
+                         ((pslot ^ d3key(rr)) << 4));
+    }
+    dma_pieces<PB, NW>(wsrd, bring + (q % STAGES) * TILE_B, vo, 0, wave);
+  };
+#pragma unroll
+  for (int q = 0; q < PD; ++q) issue_w(q);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+  __builtin_amdgcn_s_barrier();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  int qbase[TM];  // window row of this lane's output position at offset (0, 0)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wm * WM + 16 * i + fr;
+    qbase[i] = (m / TW) * WWID + (m % TW);
+  }
+  int poff[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int row = wn * WN + 16 * j + fr;
+    poff[j] = row * ROWB + ((fq ^ d3key(row)) << 4);
+  }
+  f32x4 acc[TN][TM];
+  const int H = 2 * a.Ho, W = 2 * a.Wo;
+  bf16* __restrict__ out = (bf16*)a.dx;
+
+  int q = 0;
+#pragma unroll
+  for (int cl = 0; cl < 4; ++cl) {
+    const int ph = cl >> 1, pw = cl & 1, Sc = 1 + pw, nt = s2_ntaps(cl);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int cc = 0; cc < NCH; ++cc) {
+      const char* win = smem + cc * WIN;
+      for (int tt = 0; tt < nt; ++tt, ++q) {
+        issue_w(q + PD);
+        const int t = tt / Sc, u = tt - t * Sc;
+        const int toff = (ph - t) * WWID + (pw - u);
+        const char* bst = bring + (q % STAGES) * TILE_B;
+        int qoff[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = qbase[i] + toff;
+          qoff[i] = row * ROWB + ((fq ^ d3key(row)) << 4);
+        }
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          bf16x8 pf[TN], qf[TM];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(bst + (poff[j] ^ (sub << 6)));
+#pragma unroll
+          for (int i = 0; i < TM; ++i) qf[i] = *(const bf16x8*)(win + (qoff[i] ^ (sub << 6)));
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
+        }
+        // weight tile q+1 landed (tiles q+2 .. q+PD stay in flight) for every wave
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    // class epilogue: lane holds dX[2(i0+pi)+ph][2(j0+pj)+pw][n..n+3]
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = wm * WM + 16 * i + fr;
+      const int hi = i0 + m / TW, wj = j0 + m % TW;
+      if (hi >= a.Ho || wj >= a.Wo) continue;
+      const size_t pix = ((size_t)img * H + 2 * hi + ph) * W + 2 * wj + pw;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + 16 * j + 4 * fq;
+        if (n < a.C) store4(out + pix * a.C + n, acc[j][i]);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail loads
+}
+
 // ============================================================================ weight gradient
 // dW[k][tap][c] = sum_p dY[p][k] * X[p + shift(tap)][c] over the pixels of the split.  A
 // workgroup owns a 64 (k) x 64 (c) x 9 (taps) output block and walks its split's pixel chunks
@@ -865,6 +1029,57 @@ bool pick(int N, int H, int W, int Cin, int Nout, D3Cfg* out) {
   return false;
 }
 }  // namespace
+
+namespace {
+bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) {
+  if (K % 64 || C % 64) return false;
+  *nch = K / 64;
+  if (Wo == 32 && Ho % 8 == 0 && C == 64 && K == 128) {  // layer 2
+    *TH = 8; *TW = 32; *BN = 64;
+    return true;
+  }
+  if (Wo == 16 && Ho % 8 == 0 && C == 128 && K == 256) {  // layer 3
+    *TH = 8; *TW = 16; *BN = 64;
+    return true;
+  }
+  return false;
+}
+}  // namespace
+
+int conv3s2_dgrad_launch(const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho, int Wo,
+                         int K, int C, hipStream_t st) {
+  if (g_direct == 0) return 1;
+  int TH, TW, BN, nch;
+  if (!s2_pick(Ho, Wo, K, C, &TH, &TW, &BN, &nch)) return 1;
+  const size_t dybytes = (size_t)N * Ho * Wo * K * 2, wbytes = (size_t)9 * C * K * 2;
+  if (dybytes >= (1u << 31) || (size_t)N * 4 * Ho * Wo * C * 2 >= (1u << 31)) return 1;
+  D3S2Args a;
+  a.dy = dy;
+  a.w = w_cls;
+  a.dx = dx;
+  a.N = N;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.K = K;
+  a.C = C;
+  a.tiles_x = Wo / TW;
+  a.tiles_per_img = (Ho / TH) * a.tiles_x;
+  a.ntn = C / BN;
+  for (int i = 0; i < 4; ++i) a.cls_off[i] = cls_off[i];
+  a.dybytes = (uint32_t)dybytes;
+  a.wbytes = (uint32_t)wbytes;
+  const int ntm = N * a.tiles_per_img;
+  const dim3 grid(ntm * a.ntn);
+  probe_begin(st);
+  if (nch == 2)
+    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 32, 64, 4, 2, 2, 3>), grid, dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
+  probe_end(st);
+  SQR_HIP_LAUNCH_CHECK("conv3s2_dgrad_kernel");
+  return 0;
+}
+
 
 // 1 = not applicable (caller falls back to the implicit-GEMM path), 0 = launched, else error
 int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,

@@ -76,6 +76,10 @@ __device__ __forceinline__ int tn_swz(int row, int win) {
 // path), 0 = launched, otherwise an error code
 int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st);
+// direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
+// packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): 1 = not handled
+int conv3s2_dgrad_launch(const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho, int Wo,
+                         int K, int C, hipStream_t st);
 // direct 3x3/s1/p1 bf16 weight gradient: fp32 slabs [splits][K][9*C] ((tap, c) columns, the
 // implicit-GEMM TN layout) for wgrad_reduce_kernel.  conv3w_slab_bytes = 0 if not handled.
 size_t conv3w_slab_bytes(int N, int H, int W, int C, int K);

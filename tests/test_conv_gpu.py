@@ -201,3 +201,34 @@ def test_conv3_persistent_bands(N):
     yd = y1.double()
     assert _rel(st1[0], yd.sum((0, 2, 3))) <= 1e-5
     assert _rel(st1[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 128), (3, 128, 32, 256), (64, 64, 64, 128), (64, 128, 32, 256)],
+                         ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv3s2_dgrad_direct(shape):
+    """Direct stride-2 backward-data kernel (layers 2-3 first convs: all four parity classes in one
+    launch) against the float64 reference (small N) and the parity-class implicit GEMM (mode 0)."""
+    from sqr import conv as sc
+    from sqr._lib import lib
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(7 * N + C + K)
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    gy = torch.randn(N, K, H // 2, H // 2, generator=g).bfloat16().float()
+    d = sc._desc(N, C, H, H, K, 3, 3, 2, 1, torch.bfloat16)
+    _, crsk = sc.pack_weight(w.to(DEV), d, True)
+    gyg = gy.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    res = {}
+    old = lib().sqr_conv_set_direct(1)
+    try:
+        for mode in (1, 0):
+            lib().sqr_conv_set_direct(mode)
+            res[mode] = sc.conv2d_bwd_data(gyg, crsk, d).float()
+            torch.cuda.synchronize()
+    finally:
+        lib().sqr_conv_set_direct(old)
+    assert _rel(res[1], res[0]) <= 8e-3
+    assert (res[1] - res[0]).abs().max().item() <= 0.02 * res[0].abs().max().item()
+    if N <= 4:
+        x = torch.zeros(N, C, H, H)
+        _, dxr, _ = _ref(x, w.bfloat16().float(), 2, 1, gy)
+        assert _rel(res[1], dxr) <= 8e-3
