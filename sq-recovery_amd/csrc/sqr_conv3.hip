@@ -616,9 +616,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   constexpr int NSTEP = 9 * NCH;
   static_assert(PB >= 1 && PB * 8 * NW == BN, "BN must be a multiple of 8 * waves");
   static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0, "wave tile");
-  static_assert(PB * (PD - 1) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(1024))) char smem[NCH * WIN + STAGES * TILE_B];
-  char* const bring = smem + NCH * WIN;
+  constexpr int NWIN = NCH < 2 ? 1 : 2;  // double-buffered dY windows (chunk cc in slot cc & 1)
+  static_assert(PB * (PD - 1) + WP <= 63, "vmcnt range");
+  static_assert(PD <= 8, "the next window must land within its chunk's 9 steps");
+  __shared__ __attribute__((aligned(1024))) char smem[NWIN * WIN + STAGES * TILE_B];
+  char* const bring = smem + NWIN * WIN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -633,9 +635,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   const __amdgpu_buffer_rsrc_t dsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, a.dybytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, a.wbytes, 0x00020000);
 
-  // dY windows of all chunks: window row r = (y, x) -> dY position (i0 + y, j0 + x)
+  // dY window of a chunk: window row r = (y, x) -> dY position (i0 + y, j0 + x)
+  uint32_t wvoff[WP];
   {
-    uint32_t wvoff[WP];
 #pragma unroll
     for (int i = 0; i < WP; ++i) {
       const int r = (i * NW + wave) * 8 + prow;
@@ -644,22 +646,21 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
       const bool ok = r < WR && h < a.Ho && w < a.Wo;
       wvoff[i] = ok ? (uint32_t)((((img * a.Ho + h) * a.Wo + w) * a.K) * 2 + ((pslot ^ d3key(r)) << 4)) : kOOB;
     }
-#pragma unroll
-    for (int cc = 0; cc < NCH; ++cc)
-      dma_pieces<WP, NW>(dsrd, smem + cc * WIN, wvoff, __builtin_amdgcn_readfirstlane(cc * 128), wave);
   }
-  // weight tile of step q: class cl, chunk cc, tap tt -> rows c = n0 + row of class cl
+  auto issue_win = [&](int cc) {
+    dma_pieces<WP, NW>(dsrd, smem + (cc & 1) * WIN, wvoff, __builtin_amdgcn_readfirstlane(cc * 128), wave);
+  };
+  issue_win(0);
+  // weight tile of step q = 9 cc + s: chunk cc, class cl, tap tt (s = class offset + tt) -> rows
+  // c = n0 + row of class cl
   int wrow[PB];
 #pragma unroll
   for (int i = 0; i < PB; ++i) wrow[i] = n0 + (i * NW + wave) * 8 + prow;
   auto issue_w = [&](int q) {
     q = q < NSTEP ? q : NSTEP - 1;  // dummy reloads past the end keep the per-wave counts uniform
-    int cl = 0, rem = q;
-    while (rem >= s2_ntaps(cl) * NCH) {
-      rem -= s2_ntaps(cl) * NCH;
-      ++cl;
-    }
-    const int nt = s2_ntaps(cl), cc = rem / nt, tt = rem - cc * nt;
+    const int cc = q / 9, s = q - 9 * cc;
+    const int cl = s < 1 ? 0 : (s < 3 ? 1 : (s < 5 ? 2 : 3));
+    const int nt = s2_ntaps(cl), tt = s - (cl == 0 ? 0 : (cl == 1 ? 1 : (cl == 2 ? 3 : 5)));
     uint32_t vo[PB];
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
@@ -667,6 +668,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
       vo[i] = (uint32_t)(((size_t)a.cls_off[cl] + ((size_t)wrow[i] * nt + tt) * a.K + cc * 64) * 2 +
                          ((pslot ^ d3key(rr)) << 4));
     }
+#if SQR_EXP & 8192
+    if (q >= PD) return;
+#endif
     dma_pieces<PB, NW>(wsrd, bring + (q % STAGES) * TILE_B, vo, 0, wave);
   };
 #pragma unroll
@@ -687,22 +691,28 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
     const int row = wn * WN + 16 * j + fr;
     poff[j] = row * ROWB + ((fq ^ d3key(row)) << 4);
   }
-  f32x4 acc[TN][TM];
-  const int H = 2 * a.Ho, W = 2 * a.Wo;
-  bf16* __restrict__ out = (bf16*)a.dx;
-
-  int q = 0;
+  // all four classes stay in registers to the end: a per-class epilogue would write every other
+  // pixel (partial lines) and its stores would hold up the next class's vmcnt waits
+  f32x4 acc[4][TN][TM];
 #pragma unroll
-  for (int cl = 0; cl < 4; ++cl) {
-    const int ph = cl >> 1, pw = cl & 1, Sc = 1 + pw, nt = s2_ntaps(cl);
+  for (int cl = 0; cl < 4; ++cl)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int cc = 0; cc < NCH; ++cc) {
-      const char* win = smem + cc * WIN;
+      for (int i = 0; i < TM; ++i) acc[cl][j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int q = 0;
+  for (int cc = 0; cc < NCH; ++cc) {
+    const char* win = smem + (cc & 1) * WIN;
+    const bool next_win = cc + 1 < NCH;
+#pragma unroll
+    for (int cl = 0; cl < 4; ++cl) {
+      const int ph = cl >> 1, pw = cl & 1, Sc = 1 + pw, nt = s2_ntaps(cl);
+#pragma unroll
       for (int tt = 0; tt < nt; ++tt, ++q) {
         issue_w(q + PD);
+        // chunk cc + 1's window into the slot chunk cc - 1 used (every wave is past it)
+        if (cl == 0 && next_win) issue_win(cc + 1);
         const int t = tt / Sc, u = tt - t * Sc;
         const int toff = (ph - t) * WWID + (pw - u);
         const char* bst = bring + (q % STAGES) * TILE_B;
@@ -722,25 +732,67 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
+            for (int i = 0; i < TM; ++i) {
+#if SQR_EXP & 4096
+              acc[cl][j][i][0] += (float)pf[j][0] * (float)qf[i][0];
+#else
+              acc[cl][j][i] = mfma(pf[j], qf[i], acc[cl][j][i]);
+#endif
+            }
         }
-        // weight tile q+1 landed (tiles q+2 .. q+PD stay in flight) for every wave
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+        // weight tile q+1 landed (tiles q+2 .. q+PD stay in flight; so does the next window while
+        // it is younger than tile q+1, i.e. for the first PD-1 steps of the chunk)
+        const int s = q - 9 * cc;
+        if (next_win && s <= PD - 2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1) + WP) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
         __builtin_amdgcn_s_barrier();
       }
     }
-    // class epilogue: lane holds dX[2(i0+pi)+ph][2(j0+pj)+pw][n..n+3]
+  }
+  // epilogue, one output-row parity at a time: classes (ph, 0) and (ph, 1) interleave into a
+  // [TH][2TW][BN] staging tile in the (now dead) window LDS, copied out as full 16-B pieces of
+  // contiguous pixel rows.  Staging slot key (p >> 1) & 7 spreads a class's stride-2 pixels.
+  constexpr int SL = BN / 8, PX = 2 * TW, HALF = TH * PX * SL;
+  static_assert(TH * PX * BN * 2 <= NWIN * WIN + STAGES * TILE_B, "staging tile fits the LDS");
+  if (TH * PX * BN * 2 > NWIN * WIN) {  // staging overlaps the weight ring: its dummy tail loads first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  static_assert(SL >= 8, "staging swizzle assumes at least 8 slots per pixel");
+  const int H = 2 * a.Ho, W = 2 * a.Wo;
+  bf16* __restrict__ out = (bf16*)a.dx;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = wm * WM + 16 * i + fr;
-      const int hi = i0 + m / TW, wj = j0 + m % TW;
-      if (hi >= a.Ho || wj >= a.Wo) continue;
-      const size_t pix = ((size_t)img * H + 2 * hi + ph) * W + 2 * wj + pw;
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph) __syncthreads();  // previous half copied out
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WN + 16 * j + 4 * fq;
-        if (n < a.C) store4(out + pix * a.C + n, acc[j][i]);
+    for (int pw = 0; pw < 2; ++pw)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = wm * WM + 16 * i + fr;
+        const int p = (m / TW) * PX + 2 * (m % TW) + pw;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = wn * WN + 16 * j + 4 * fq;
+          const int slot = (n >> 3) ^ ((p >> 1) & 7);
+#if SQR_EXP & 2048
+          if (acc[2 * ph + pw][j][i][0] == 1.2345f)
+#endif
+          store4((bf16*)(smem + p * (BN * 2) + slot * 16 + (n & 4) * 2), acc[2 * ph + pw][j][i]);
+        }
       }
+    __syncthreads();
+    for (int idx = tid; idx < HALF; idx += 64 * NW) {
+      const int p = idx / SL, sl = idx - p * SL;
+      const int y = p / PX, x = p - y * PX;
+      if (i0 + y >= a.Ho || j0 + (x >> 1) >= a.Wo) continue;
+      const uint4 v = *(const uint4*)(smem + p * (BN * 2) + ((sl ^ ((p >> 1) & 7)) << 4));
+      const size_t pix = ((size_t)img * H + 2 * (i0 + y) + ph) * W + 2 * j0 + x;
+#if SQR_EXP & 2048
+      if (v.x == 12345u)
+#endif
+      *(uint4*)(out + pix * a.C + n0 + 8 * sl) = v;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail loads
@@ -1034,12 +1086,12 @@ namespace {
 bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) {
   if (K % 64 || C % 64) return false;
   *nch = K / 64;
-  if (Wo == 32 && Ho % 8 == 0 && C == 64 && K == 128) {  // layer 2
+  if (Wo == 32 && Ho % 8 == 0 && C == 64 && K == 128) {  // layer 2 (tiles must match the launches below)
     *TH = 8; *TW = 32; *BN = 64;
     return true;
   }
   if (Wo == 16 && Ho % 8 == 0 && C == 128 && K == 256) {  // layer 3
-    *TH = 8; *TW = 16; *BN = 64;
+    *TH = 4; *TW = 16; *BN = 64;
     return true;
   }
   return false;
@@ -1068,13 +1120,14 @@ int conv3s2_dgrad_launch(const void* dy, const void* w_cls, const int* cls_off, 
   for (int i = 0; i < 4; ++i) a.cls_off[i] = cls_off[i];
   a.dybytes = (uint32_t)dybytes;
   a.wbytes = (uint32_t)wbytes;
-  const int ntm = N * a.tiles_per_img;
-  const dim3 grid(ntm * a.ntn);
+  // measured (N=64, rocprofv3): layer 2 17.9 us (8x32 tile, 5-deep weight ring, 8 waves), layer 3
+  // 17.6 us (4x16 tile, two workgroups per CU); 4x32 / 8x16 / BN 128 / 2x2-wave variants were slower
+  const dim3 grid(N * a.tiles_per_img * a.ntn);
   probe_begin(st);
   if (nch == 2)
-    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 32, 64, 4, 2, 2, 3>), grid, dim3(512), 0, st, a);
+    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 32, 64, 4, 2, 2, 5>), grid, dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv3s2_dgrad_kernel<4, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3s2_dgrad_kernel");
   return 0;
