@@ -1094,6 +1094,10 @@ bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) 
     *TH = 4; *TW = 16; *BN = 64;
     return true;
   }
+  if (Wo == 8 && Ho % 8 == 0 && C == 256 && K == 512) {  // layer 4
+    *TH = 8; *TW = 8; *BN = 64;
+    return true;
+  }
   return false;
 }
 }  // namespace
@@ -1121,11 +1125,15 @@ int conv3s2_dgrad_launch(const void* dy, const void* w_cls, const int* cls_off, 
   a.dybytes = (uint32_t)dybytes;
   a.wbytes = (uint32_t)wbytes;
   // measured (N=64, rocprofv3): layer 2 17.9 us (8x32 tile, 5-deep weight ring, 8 waves), layer 3
-  // 17.6 us (4x16 tile, two workgroups per CU); 4x32 / 8x16 / BN 128 / 2x2-wave variants were slower
+  // 17.6 us (4x16 tile, two workgroups per CU), layer 4 20.0 us (one 8x8 image per tile; the
+  // implicit GEMM: 39.6 / 23.2 / 23.7 us); 4x32 / 8x16 / BN 128 / 2x2-wave / deeper-ring variants were
+  // slower
   const dim3 grid(N * a.tiles_per_img * a.ntn);
   probe_begin(st);
   if (nch == 2)
     hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 32, 64, 4, 2, 2, 5>), grid, dim3(512), 0, st, a);
+  else if (nch == 8)
+    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 8, 64, 2, 2, 8, 3>), grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((conv3s2_dgrad_kernel<4, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
   probe_end(st);

@@ -203,10 +203,11 @@ def test_conv3_persistent_bands(N):
     assert _rel(st1[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 64, 128), (3, 128, 32, 256), (64, 64, 64, 128), (64, 128, 32, 256)],
+@pytest.mark.parametrize("shape", [(2, 64, 64, 128), (3, 128, 32, 256), (3, 256, 16, 512), (64, 64, 64, 128),
+                                   (64, 128, 32, 256), (64, 256, 16, 512)],
                          ids=lambda s: "N%dC%dH%dK%d" % s)
 def test_conv3s2_dgrad_direct(shape):
-    """Direct stride-2 backward-data kernel (layers 2-3 first convs: all four parity classes in one
+    """Direct stride-2 backward-data kernel (layers 2-4 first convs: all four parity classes in one
     launch) against the float64 reference (small N) and the parity-class implicit GEMM (mode 0)."""
     from sqr import conv as sc
     from sqr._lib import lib
