@@ -134,15 +134,17 @@ int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_de
  * sqr_stem_fwd_stats so the BatchNorm that follows the conv never re-reads the activation. */
 size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
 /* Routing of bf16 3x3/stride-1/pad-1 forward and backward-data convs to the direct halo-window
- * kernels (C = K = 64, W = 64: the persistent resident-weight kernel; otherwise the tiled one):
- * 1 (default) when the shape tiles and the grid fills the chip, 2 whenever the shape tiles,
- * 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.
+ * kernels (C = K = 64, W = 64: the persistent resident-weight kernel; otherwise the tiled one),
+ * and of bf16 3x3/stride-2/pad-1 backward-data convs of ResNetSQ's layer 2-4 shapes to the direct
+ * parity-class kernel: 1 (default) when the shape tiles and the grid fills the chip (stride 2:
+ * whenever it tiles), 2 whenever the shape tiles, 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.
  * Process-wide; meant for A/B tests. */
 int sqr_conv_set_direct(int mode);
 int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
                          int* stats_rows, void* workspace, size_t workspace_bytes, void* stream);
 /* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1
- * implicit GEMM per output-parity class (no work on structurally zero taps). */
+ * implicit GEMM per output-parity class (no work on structurally zero taps), all classes in one
+ * launch; bf16 3x3/s2 shapes of ResNetSQ's layers 2-4 take the direct window kernel instead. */
 int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
                         void* workspace, size_t workspace_bytes, void* stream);
 /* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
