@@ -26,7 +26,8 @@
 #define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop;
                    // conv3_kernel: 4 no per-tap wait/barrier, 8 no MFMA, 16 no fragment reads;
                    // conv3p_kernel: 128 no tap loop, 256 no output stores, 512 no row loads in
-                   // the tile loop, 1024 no fragment reads)
+                   // the tile loop, 1024 no fragment reads; conv3s2_dgrad_kernel: 2048 no dX
+                   // stores, 4096 no MFMA, 8192 no weight loads after the prologue)
 #endif
 
 namespace sqr {
