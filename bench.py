@@ -5,7 +5,9 @@ implicit-GEMM convs, bf16 autocast), ImplicitLoss(32, tau=1.5, s=260) on the inp
 (fused HIP loss + analytic grad, fp32), backward, Adam(lr=1e-4) step (sqr.optim.Adam: the same
 update as torch.optim.Adam in libsqr's fused kernel) — plus, for N>1, DDP's bucketed RCCL
 all-reduce of the gradients overlapped with backward.  Per-GPU batch 64
-(BASELINE config 2; config 3 = 8 GPUs x 64).
+(BASELINE config 2; config 3 = 8 GPUs x 64).  `--config 4` adds ExplicitLoss(32) on the labels
+with ImplicitLoss(64); `--config 5` runs 512x512 images with ImplicitLoss(64) (in bf16; the fp16 +
+loss-scaling variant is not built).  Config 2 is the default and the metric's line.
 
 Synthetic data: SQ parameters drawn from the reference's generator distribution
 (gen_rand_rot.py:21-31) with seed 1234+rank, rendered on the GPU into 256x256 depth images with
@@ -98,7 +100,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
-    ap.add_argument("--render", type=int, default=32, help="ImplicitLoss render size R")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+                    help="BASELINE.json config: 2 = ImplicitLoss(32) at 256x256 (default, the metric's config), "
+                         "4 = ExplicitLoss(32)(labels) + ImplicitLoss(64)(images) at 256x256, "
+                         "5 = ImplicitLoss(64) at 512x512")
+    ap.add_argument("--render", type=int, default=0, help="ImplicitLoss render size R (0 = the config's)")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (0 = skip)")
     ap.add_argument("--breakdown", action="store_true", help="print a per-phase timing breakdown to stderr")
     ap.add_argument("--graph", type=int, default=-1,
@@ -119,7 +125,9 @@ def main():
     from sqr import losses
     from sqr import optim as sqr_optim
 
-    B, R, H = args.batch, args.render, 256
+    B = args.batch
+    H = 512 if args.config == 5 else 256
+    R = args.render or (32 if args.config == 2 else 64)
     rng = np.random.default_rng(1234 + rank)
     params = torch.tensor(classes.sample_sq_params(rng, B), device=dev)
     images = losses.implicit_render(params, H, 1.5, 260).unsqueeze(1).contiguous()  # [B,1,256,256] in [0,1]
@@ -130,6 +138,9 @@ def main():
     # torch.optim.Adam's semantics on libsqr's fused step (also writes the bf16 packed conv weights)
     opt = sqr_optim.Adam(net.parameters(), lr=1e-4, weight_decay=0).attach(net)
     crit = classes.ImplicitLoss(R, dev, 1.5, 260)
+    # config 4: ExplicitLoss(32)(p_true, pred) + ImplicitLoss(64)(img, pred); the
+    # labels are the parameters the synthetic images were rendered from
+    crit_x = classes.ExplicitLoss(32, dev) if args.config == 4 else None
     use_graph = args.graph != 0
     # N > 1: the graph-captured data-parallel step (flat gradient buffer + one RCCL all-reduce in the
     # graph) unless disabled; eager DDP (bucketed all-reduce overlapped with backward) otherwise
@@ -150,6 +161,8 @@ def main():
             out = model(images)
         pred = torch.cat([o.float() for o in out], dim=1)
         loss = crit(images, pred)
+        if crit_x is not None:
+            loss = loss + crit_x(params, pred)
         loss.backward()
         if gdp is not None:
             gdp.allreduce()
@@ -203,7 +216,8 @@ def main():
         step()
     barrier()
 
-    pc, ph, pr, ps = PROBE[1], PROBE[2], PROBE[3], PROBE[4]
+    # the probe follows the image size: layer1's 3x3 64->64 conv runs at H/4 x H/4
+    pc, ph, pr, ps = PROBE[1], PROBE[2] * H // 256, PROBE[3], PROBE[4]
     loss_acc = torch.zeros((), dtype=torch.float64, device=dev)
     if not use_graph:
         sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
@@ -243,40 +257,47 @@ def main():
     value = B * world * args.steps / dt
     flops = conv_flops(B, pc, ph, pc, pr, ps)
     achieved = flops / (kern_ms * 1e-3) / 1e12 if events else None
-    roof = {"bound": "mfma", "kernel": "conv_%s %dx%d %dx%d s%d (layer1 persistent direct conv, bf16)"
-                                       % (PROBE[0], pc, pc, pr, pr, ps),
+    roof = {"bound": "mfma", "kernel": "conv_%s %dx%d %dx%d s%d (layer1 %s direct conv, bf16)"
+                                       % (PROBE[0], ph, ph, pr, pr, ps,
+                                          "persistent" if ph == 64 else "tiled"),
             "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
             "kernel_ms": kern_ms, "launches": len(events), "traffic": None}
     # secondary rooflines: the whole step's conv work against the MFMA peak, and the
     # fused loss call against the transcendental rate (per voxel ~21 exp2/log2/rcp, fwd + bwd)
     loss_ms = time_loss_call(crit, images, B, dev) if rank == 0 else None
-    extra = {"conv_whole_step": {"gflop_per_image": CONV_GFLOP_PER_IMG,
-                                 "achieved": value * CONV_GFLOP_PER_IMG / 1e3, "peak": PEAK_BF16_TFLOPS,
+    gflop_img = CONV_GFLOP_PER_IMG * (H // 256) ** 2  # 53.97 at 512x512 (§8(d)); conv1 scales the same
+    extra = {"conv_whole_step": {"gflop_per_image": gflop_img,
+                                 "achieved": value * gflop_img / 1e3, "peak": PEAK_BF16_TFLOPS,
                                  "unit": "TFLOP/s",
-                                 "frac": value * CONV_GFLOP_PER_IMG / 1e3 / PEAK_BF16_TFLOPS}}
+                                 "frac": value * gflop_img / 1e3 / PEAK_BF16_TFLOPS}}
     if loss_ms:
         tps = B * R ** 3 * LOSS_TRANSC_PER_VOXEL / (loss_ms * 1e-3) / 1e12
         extra["implicit_loss"] = {"call_ms_graph": loss_ms, "achieved": tps, "peak": PEAK_TRANSC_TPS,
                                   "unit": "T transcendentals/s", "frac": tps / PEAK_TRANSC_TPS,
                                   "hbm_bytes_per_image": R * R * 4 + 96}
     tr = load_traffic()
-    if tr and tr.get("kernel_key") == list(PROBE):
+    if tr and tr.get("kernel_key") == list(PROBE) and H == 256:
         roof["traffic"] = tr.get("hbm_bytes_per_launch")
 
-    out = {"metric": "training images/sec (256x256 depth, implicit loss)", "value": value, "unit": "images/s",
+    workload = {2: "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
+                4: "ResNetSQ + ExplicitLoss(R=32)(labels) + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
+                5: "ResNetSQ at 512x512 + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam (bf16: no loss "
+                   "scaling needed; the fp16 variant of config 5 is not built)" % R}[args.config]
+    out = {"metric": "training images/sec (%dx%d depth, %s loss)" % (H, H, "explicit+implicit" if crit_x else "implicit"),
+           "value": value, "unit": "images/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
            "data": "synthetic (GPU-rendered SQ depth images, reference label distribution)",
-           "config": {"workload": "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
+           "config": {"workload": workload, "baseline_config": args.config,
                       "model": "ResNetSQ (resnet18 backbone, 11.37M params)", "global_batch": B * world,
-                      "per_gpu_batch": B, "image": "256x256x1", "render_size": R,
+                      "per_gpu_batch": B, "image": "%dx%dx1" % (H, H), "render_size": R,
                       "parallelism": "dp%d" % world},
            "mean_loss": mean_loss, "hip_graph": use_graph,
            "dp": ("graph-captured RCCL all-reduce" if gdp is not None else ("DDP" if world > 1 else None)),
            "roofline": roof, "roofline_extra": extra}
 
-    if rank == 0 and world == 1 and args.cpu_steps > 0:
+    if rank == 0 and world == 1 and args.cpu_steps > 0 and args.config == 2:
         imgs_cpu = images.detach().cpu()
         v, secs = cpu_baseline(imgs_cpu, state0, R, args.cpu_steps)
         out["cpu_baseline"] = {"value": v, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
