@@ -1,17 +1,20 @@
 """Training throughput of the sq-recovery hot path on MI355X (BASELINE.json metric).
 
 One step = torch/train.py's step (train.py:86-103) on a synthetic batch: ResNetSQ forward (HIP
-implicit-GEMM convs, bf16 autocast), ImplicitLoss(32, tau=1.5, s=260) on the input depth images
-(fused HIP loss + analytic grad, fp32), backward, Adam(lr=1e-4) step (sqr.optim.Adam: the same
-update as torch.optim.Adam in libsqr's fused kernel) — plus, for N>1, DDP's bucketed RCCL
-all-reduce of the gradients overlapped with backward.  Per-GPU batch 64
-(BASELINE config 2; config 3 = 8 GPUs x 64).  `--config 4` adds ExplicitLoss(32) on the labels
-with ImplicitLoss(64); `--config 5` runs 512x512 images with ImplicitLoss(64) (in bf16; the fp16 +
-loss-scaling variant is not built).  Config 2 is the default and the metric's line.
+convs under autocast), ImplicitLoss(R, tau=1.5, s=260) on the input depth images (fused HIP loss +
+analytic grad, fp32), backward, Adam(lr=1e-4) step (sqr.optim.Adam: the same update as
+torch.optim.Adam in libsqr's fused kernel) — plus, for N>1, the bucketed RCCL all-reduce of the
+gradients overlapped with backward.  The whole step is captured in ONE HIP graph and replayed.
+
+BASELINE.json configs (per-GPU batch 64):
+  --config 2  ImplicitLoss(32), 256x256, bf16                      (default: the metric's line)
+  --config 3  = config 2 launched on 8 GPUs (torchrun) — weak scaling, global batch 512
+  --config 4  ExplicitLoss(32)(labels, pred) + ImplicitLoss(64)(images, pred), 256x256, bf16
+  --config 5  ImplicitLoss(64), 512x512, fp16 + dynamic loss scaling (sqr.amp.GradScaler)
 
 Synthetic data: SQ parameters drawn from the reference's generator distribution
-(gen_rand_rot.py:21-31) with seed 1234+rank, rendered on the GPU into 256x256 depth images with
-the same inside-outside model (values in [0,1], background 0).
+(gen_rand_rot.py:21-31) with seed 1234+rank, rendered on the GPU into HxH depth images with the
+same inside-outside model (values in [0,1], background 0).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -21,6 +24,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -30,14 +34,15 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sq-recovery_amd"))
 
-PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_MFMA_TFLOPS = 2500.0  # MI355X dense bf16 / fp16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
 
-# dominant kernel (largest share of step time in profiles/): the layer1 3x3 64->64 convs
 CONV_GFLOP_PER_IMG = 13.49  # ResNetSQ fwd + dgrad + wgrad per 256x256 image
 LOSS_TRANSC_PER_VOXEL = 21  # ImplicitLoss fwd (~13) + bwd (~8) transcendentals per voxel (§8(d))
 PEAK_TRANSC_TPS = 9.8       # 256 CU x 16 transcendentals/clk x 2.4 GHz (§8(d), datasheet-derived)
-PROBE = ("fwd", 64, 64, 3, 1)  # phase, C, H(=W), R, stride  (N = per-GPU batch): layer-1 3x3 conv
+# dominant kernel (largest share of the step in profiles/): layer1's 3x3 64->64 forward conv
+PROBE = ("fwd", 64, 64, 3, 1)  # phase, C, H(=W) at 256x256 input, R, stride  (N = per-GPU batch)
+N_PROBE_SLOTS = 64
 
 
 def conv_flops(N, C, H, K, R, stride):
@@ -46,21 +51,182 @@ def conv_flops(N, C, H, K, R, stride):
     return 2.0 * N * Ho * Ho * K * C * R * R
 
 
-def cpu_baseline(images_cpu, state_dict, R, steps):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ref_torch
-    torch.set_num_threads(max(1, torch.get_num_threads()))
-    net = ref_torch.ResNetSQRef()
-    missing = net.load_state_dict(state_dict, strict=False)
-    assert not missing.missing_keys, missing.missing_keys
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-    crit = ref_torch.ImplicitLossRef(R, 1.5, 260)
-    ref_torch.train_step(net, opt, crit, images_cpu)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ref_torch.train_step(net, opt, crit, images_cpu)
-    dt = time.perf_counter() - t0
-    return images_cpu.shape[0] * steps / dt, dt
+def config_shape(config, render=0):
+    """(H, R, compute dtype) of a BASELINE.json config."""
+    H = 512 if config == 5 else 256
+    R = render or (32 if config in (2, 3) else 64)
+    return H, R, (torch.float16 if config == 5 else torch.bfloat16)
+
+
+class Trainer:
+    """bench.py's training step (also imported by tests/test_step_gpu.py, which checks exactly this
+    step's gradients against a float64 reference)."""
+
+    def __init__(self, dev, config=2, batch=64, render=0, dtype=None, graph=True, rank=0, world=1, seed=1234):
+        import classes
+        import models
+        from sqr import amp, dist
+        from sqr import losses
+        from sqr import optim as sqr_optim
+        self.dev, self.config, self.B, self.world = dev, config, batch, world
+        self.H, self.R, cdt = config_shape(config, render)
+        self.dtype = dtype or cdt
+        rng = np.random.default_rng(seed + rank)
+        self.params = torch.tensor(classes.sample_sq_params(rng, batch), device=dev)
+        # [B,1,H,H] in [0,1]
+        self.images = losses.implicit_render(self.params, self.H, 1.5, 260).unsqueeze(1).contiguous()
+
+        torch.manual_seed(0)  # identical init on every rank (the data-parallel wrappers also broadcast)
+        self.net = models.ResNetSQ(outputs=4, pretrained=False).to(dev)
+        self.state0 = {k: v.detach().cpu().clone() for k, v in self.net.state_dict().items()}
+        # torch.optim.Adam's semantics on libsqr's fused step (also writes the packed conv weights)
+        self.opt = sqr_optim.Adam(self.net.parameters(), lr=1e-4, weight_decay=0).attach(self.net, self.dtype)
+        self.crit = classes.ImplicitLoss(self.R, dev, 1.5, 260)
+        # config 4 (SURVEY.md §8(d)): ExplicitLoss(32)(p_true, pred) + ImplicitLoss(64)(img, pred); the
+        # labels are the parameters the synthetic images were rendered from
+        self.crit_x = classes.ExplicitLoss(32, dev) if config == 4 else None
+        # fp16: dynamic loss scaling (GradScaler semantics, device-resident, graph-capturable)
+        self.scaler = amp.GradScaler() if self.dtype == torch.float16 else None
+        self.use_graph = graph
+        self.gdp = None
+        self.model = self.net
+        force_dp = os.environ.get("SQR_DP_FORCE", "0") == "1"  # N=1 rehearsal of the N>1 path (world-1 RCCL)
+        if force_dp and world == 1 and not torch.distributed.is_initialized():
+            torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get(
+                "MASTER_PORT", "29517"), rank=0, world_size=1, device_id=dev)
+        if (world > 1 or force_dp) and graph and os.environ.get("SQR_DP_GRAPH", "1") == "1":
+            self.gdp = dist.GraphDataParallel(self.net, self.opt, dev)
+        elif world > 1:
+            self.model = dist.wrap(self.net, dev)
+            self.use_graph = False
+        self.dp_note = None
+        self.graph = None
+        self.static_loss = None
+        self._step = self.eager_step
+
+    def forward_loss(self):
+        with torch.autocast("cuda", dtype=self.dtype):
+            out = self.model(self.images)
+        pred = torch.cat([o.float() for o in out], dim=1)
+        loss = self.crit(self.images, pred)
+        if self.crit_x is not None:
+            loss = loss + self.crit_x(self.params, pred)
+        return loss, pred
+
+    def body(self):
+        loss, _ = self.forward_loss()
+        (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
+        if self.gdp is not None:
+            self.gdp.allreduce()
+        if self.scaler is not None:
+            self.scaler.step(self.opt)
+            self.scaler.update()
+        else:
+            self.opt.step()
+        return loss.detach()
+
+    def eager_step(self):
+        self.opt.zero_grad(set_to_none=True)
+        return self.body()
+
+    def capture(self, probe_clock=None):
+        """Warm up eagerly on a side stream, then capture body() as one HIP graph.  probe_clock: an
+        int64 [n, 2] device tensor; the probed conv's launches captured in the graph record their
+        wall-clock spans into its rows on every replay (sqr_probe_arm_clock)."""
+        from sqr import conv as sconv
+        from sqr import dist
+        if not self.use_graph:
+            return
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                self.eager_step()
+                if self.gdp is not None:
+                    self.gdp.check_grads()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        self.opt.zero_grad(set_to_none=True)
+        if probe_clock is not None:
+            sconv.set_probe(*self.probe_key(), clock=probe_clock)
+        try:
+            with torch.cuda.graph(graph):
+                self.static_loss = self.body()
+        except Exception as e:  # N > 1 only: keep the run alive on eager DDP (reported in "dp")
+            if self.gdp is None:
+                raise
+            self.dp_note = "capturing the data-parallel step failed (%s: %s); eager DDP instead" % (
+                type(e).__name__, e)
+            print("bench: " + self.dp_note, file=sys.stderr)
+            torch.cuda.synchronize()
+            self.gdp.close(self.opt)
+            self.gdp = None
+            self.model = dist.wrap(self.net, self.dev)
+            self.use_graph = False
+            return
+        finally:
+            if probe_clock is not None:
+                self.probe_rows = sconv.probe_clock_rows()
+                self.probe_clock = probe_clock
+                sconv.set_probe(None, 0, 0, 0, 0, 0, 0)
+        self.graph = graph
+        self._step = self.graph_step
+
+    def graph_step(self):
+        self.graph.replay()
+        return self.static_loss
+
+    def step(self):
+        return self._step()
+
+    def probe_key(self):
+        ph = PROBE[2] * self.H // 256  # layer1 runs at H/4 x H/4
+        return (PROBE[0], self.B, PROBE[1], ph, PROBE[1], PROBE[3], PROBE[4])
+
+    def probe_flops(self):
+        _, N, C, H, K, R, s = self.probe_key()
+        return conv_flops(N, C, H, K, R, s)
+
+
+def _clock_spans_ms(clk, rows):
+    """Kernel spans (ms) recorded in the first `rows` clock-probe rows (unset rows skipped)."""
+    import ctypes
+    from sqr._lib import check, lib
+    khz = ctypes.c_int()
+    check(lib().sqr_wall_clock_khz(ctypes.byref(khz)), "sqr_wall_clock_khz")
+    d = clk[:rows].cpu()
+    ok = (d[:, 0] != -1) & (d[:, 1] > 0)
+    return [float(v) / khz.value for v in (d[ok, 1] - d[ok, 0]).tolist()]
+
+
+def _clock_reset(clk):
+    clk[:, 0].fill_(-1)  # UINT64_MAX: the kernel's first workgroup takes the atomic min
+    clk[:, 1].zero_()
+
+
+def time_probe(tr, reps=10):
+    """Mean duration of the probed conv kernel, from the kernel's own wall-clock span (first
+    workgroup start -> last workgroup end, sqr_probe_arm_clock).  Graph mode: the launches captured
+    in the step graph, over `reps` synchronised replays — the kernel exactly as it runs in the timed
+    step.  Eager mode: the same over `reps` eager steps."""
+    from sqr import conv as sconv
+    times = []
+    if tr.graph is not None and getattr(tr, "probe_rows", 0):
+        for _ in range(reps):
+            _clock_reset(tr.probe_clock)
+            tr.graph.replay()
+            torch.cuda.synchronize()
+            times += _clock_spans_ms(tr.probe_clock, tr.probe_rows)
+        return (float(np.mean(times)) if times else float("nan")), len(times), "kernel wall clock, in the step graph"
+    clk = torch.empty(N_PROBE_SLOTS, 2, dtype=torch.int64, device=tr.dev)
+    _clock_reset(clk)
+    sconv.set_probe(*tr.probe_key(), clock=clk)
+    for _ in range(reps):
+        tr.eager_step()
+    torch.cuda.synchronize()
+    times = _clock_spans_ms(clk, sconv.probe_clock_rows())
+    sconv.set_probe(None, 0, 0, 0, 0, 0, 0)
+    return (float(np.mean(times)) if times else float("nan")), len(times), "kernel wall clock, eager steps"
 
 
 def time_loss_call(crit, images, B, dev, reps=20):
@@ -86,12 +252,48 @@ def time_loss_call(crit, images, B, dev, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
-def load_traffic():
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(path):
-        with open(path) as f:
-            return json.load(f)
-    return None
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(images_cpu, params_cpu, state_dict, R, steps, cfg1_steps):
+    """The reference's algorithm (oracle/ref_torch.py: stock torch CPU ops, f64 losses, Adam) timed
+    on this host: config 2's workload (ImplicitLoss(R), the same batch) and config 1 (ExplicitLoss(32)
+    on the labels, B=4, fp32 network)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_torch
+    threads = torch.get_num_threads()
+
+    def run(crit, imgs, labels, n):
+        net = ref_torch.ResNetSQRef()
+        missing = net.load_state_dict(state_dict, strict=False)
+        assert not missing.missing_keys, missing.missing_keys
+        opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+        ref_torch.train_step(net, opt, crit, imgs, labels)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(n):
+            ref_torch.train_step(net, opt, crit, imgs, labels)
+        return imgs.shape[0] * n / (time.perf_counter() - t0), time.perf_counter() - t0
+
+    v, secs = run(ref_torch.ImplicitLossRef(R, 1.5, 260), images_cpu, None, steps)
+    out = {"value": v, "unit": "images/s", "cores": threads, "kind": "port",
+           "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+           "sample": "%d train steps (1 warm-up) of batch %d: oracle/ref_torch.py ResNetSQ fp32 + "
+                     "reference-style f64 ImplicitLoss(R=%d), Adam, %d torch threads; %.1f s"
+                     % (steps, images_cpu.shape[0], R, threads, secs)}
+    if cfg1_steps > 0:
+        v1, s1 = run(ref_torch.ExplicitLossRef(32), images_cpu[:4], params_cpu[:4], cfg1_steps)
+        out["config1"] = {"value": v1, "unit": "images/s",
+                          "sample": "BASELINE config 1: %d train steps (1 warm-up) of batch 4, ResNetSQ fp32 + "
+                                    "f64 ExplicitLoss(32) on the labels, Adam; %.1f s" % (cfg1_steps, s1)}
+    return out
 
 
 def main():
@@ -100,13 +302,14 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
-                    help="BASELINE.json config: 2 = ImplicitLoss(32) at 256x256 (default, the metric's config), "
-                         "4 = ExplicitLoss(32)(labels) + ImplicitLoss(64)(images) at 256x256, "
-                         "5 = ImplicitLoss(64) at 512x512")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config (module doc)")
     ap.add_argument("--render", type=int, default=0, help="ImplicitLoss render size R (0 = the config's)")
+    ap.add_argument("--dtype", default="", choices=("", "bf16", "fp16"), help="compute dtype (default: the config's)")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (0 = skip)")
-    ap.add_argument("--breakdown", action="store_true", help="print a per-phase timing breakdown to stderr")
+    ap.add_argument("--cpu1-steps", type=int, default=5, help="timed config-1 CPU steps (0 = skip)")
+    ap.add_argument("--profile", action="store_true",
+                    help="rocprof mode: nothing runs after the timed region (no probe / loss timing / CPU "
+                         "baseline), so the last --steps step graphs of the trace are the timed ones")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole train step in a HIP graph (1/0; default: on)")
     args = ap.parse_args()
@@ -118,192 +321,89 @@ def main():
 
     from sqr import dist
     rank, world, dev = dist.init("nccl")
-
-    import classes
-    import models
-    from sqr import conv as sconv
-    from sqr import losses
-    from sqr import optim as sqr_optim
-
-    B = args.batch
-    H = 512 if args.config == 5 else 256
-    R = args.render or (32 if args.config == 2 else 64)
-    rng = np.random.default_rng(1234 + rank)
-    params = torch.tensor(classes.sample_sq_params(rng, B), device=dev)
-    images = losses.implicit_render(params, H, 1.5, 260).unsqueeze(1).contiguous()  # [B,1,256,256] in [0,1]
-
-    torch.manual_seed(0)  # identical init on every rank (the data-parallel wrappers also broadcast)
-    net = models.ResNetSQ(outputs=4, pretrained=False).to(dev)
-    state0 = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
-    # torch.optim.Adam's semantics on libsqr's fused step (also writes the bf16 packed conv weights)
-    opt = sqr_optim.Adam(net.parameters(), lr=1e-4, weight_decay=0).attach(net)
-    crit = classes.ImplicitLoss(R, dev, 1.5, 260)
-    # config 4: ExplicitLoss(32)(p_true, pred) + ImplicitLoss(64)(img, pred); the
-    # labels are the parameters the synthetic images were rendered from
-    crit_x = classes.ExplicitLoss(32, dev) if args.config == 4 else None
-    use_graph = args.graph != 0
-    # N > 1: the graph-captured data-parallel step (flat gradient buffer + one RCCL all-reduce in the
-    # graph) unless disabled; eager DDP (bucketed all-reduce overlapped with backward) otherwise
-    gdp = None
-    model = net
-    force_dp = os.environ.get("SQR_DP_FORCE", "0") == "1"  # N=1 rehearsal of the N>1 path (world-1 RCCL group)
-    if force_dp and world == 1 and not torch.distributed.is_initialized():
-        torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get(
-            "MASTER_PORT", "29517"), rank=0, world_size=1, device_id=dev)
-    if (world > 1 or force_dp) and use_graph and os.environ.get("SQR_DP_GRAPH", "1") == "1":
-        gdp = dist.GraphDataParallel(net, opt, dev)
-    elif world > 1:
-        model = dist.wrap(net, dev)
-        use_graph = False
-
-    def body():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = model(images)
-        pred = torch.cat([o.float() for o in out], dim=1)
-        loss = crit(images, pred)
-        if crit_x is not None:
-            loss = loss + crit_x(params, pred)
-        loss.backward()
-        if gdp is not None:
-            gdp.allreduce()
-        opt.step()
-        return loss.detach()
-
-    def eager_step():
-        opt.zero_grad(set_to_none=True)
-        return body()
-
-    step = eager_step
-    if use_graph:
-        # whole-step HIP graph: forward + fused loss + backward (+ all-reduce) + Adam replayed as one
-        # launch (the libsqr kernels are enqueued on torch's current stream, so they are captured too)
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(3):
-                eager_step()
-                if gdp is not None:
-                    gdp.check_grads()
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        opt.zero_grad(set_to_none=True)
-        try:
-            with torch.cuda.graph(graph):
-                static_loss = body()
-        except Exception as e:  # N > 1 only: keep the run alive on eager DDP (reported in "dp")
-            if gdp is None:
-                raise
-            print("bench: capturing the data-parallel step failed (%s: %s); eager DDP instead"
-                  % (type(e).__name__, e), file=sys.stderr)
-            torch.cuda.synchronize()
-            gdp.close(opt)
-            gdp = None
-            model = dist.wrap(net, dev)
-            use_graph = False
-            graph = None
-
-        if use_graph:
-            def graph_step():
-                graph.replay()
-                return static_loss
-            step = graph_step
+    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype)
+    tr = Trainer(dev, config=args.config, batch=args.batch, render=args.render, dtype=dtype,
+                 graph=args.graph != 0, rank=rank, world=world)
+    B, H, R = tr.B, tr.H, tr.R
+    probe_clock = None
+    if tr.use_graph and not args.profile:
+        probe_clock = torch.empty(N_PROBE_SLOTS, 2, dtype=torch.int64, device=dev)
+        _clock_reset(probe_clock)
+    tr.capture(probe_clock)
 
     def barrier():
         dist.barrier()
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        step()
+        tr.step()
     barrier()
-
-    # the probe follows the image size: layer1's 3x3 64->64 conv runs at H/4 x H/4
-    pc, ph, pr, ps = PROBE[1], PROBE[2] * H // 256, PROBE[3], PROBE[4]
-    loss_acc = torch.zeros((), dtype=torch.float64, device=dev)
-    if not use_graph:
-        sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss_acc += step()
+        loss = tr.step()
     barrier()
     dt = time.perf_counter() - t0
-    if use_graph:
-        # HIP events cannot time a kernel inside a replayed graph: time the same kernel (same
-        # shapes/inputs) over a few eager steps of the same training loop right after.
-        sconv.set_probe(PROBE[0], B, pc, ph, pc, pr, ps)
-        for _ in range(5):
-            eager_step()
-        torch.cuda.synchronize()
-    events = sconv.probe_events()
-    sconv.set_probe(None, 0, 0, 0, 0, 0, 0)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
     dt = dist.max_over_ranks(dt)
-    mean_loss = (loss_acc / args.steps).item()
-
-    if args.breakdown and rank == 0:
-        # forward / backward / optimizer split (separate, synchronised run)
-        def timed(fn, n=5):
-            torch.cuda.synchronize()
-            s = time.perf_counter()
-            for _ in range(n):
-                fn()
-            torch.cuda.synchronize()
-            return (time.perf_counter() - s) / n * 1e3
-        def fwd():
-            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-                model(images)
-        print("breakdown ms: step %.3f fwd(no-grad) %.3f" % (timed(step), timed(fwd)), file=sys.stderr)
-
+    final_loss = loss.item()
     value = B * world * args.steps / dt
-    flops = conv_flops(B, pc, ph, pc, pr, ps)
-    achieved = flops / (kern_ms * 1e-3) / 1e12 if events else None
-    roof = {"bound": "mfma", "kernel": "conv_%s %dx%d %dx%d s%d (layer1 %s direct conv, bf16)"
-                                       % (PROBE[0], ph, ph, pr, pr, ps,
-                                          "persistent" if ph == 64 else "tiled"),
-            "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
-            "kernel_ms": kern_ms, "launches": len(events), "traffic": None}
-    # secondary rooflines: the whole step's conv work against the MFMA peak, and the
-    # fused loss call against the transcendental rate (per voxel ~21 exp2/log2/rcp, fwd + bwd)
-    loss_ms = time_loss_call(crit, images, B, dev) if rank == 0 else None
-    gflop_img = CONV_GFLOP_PER_IMG * (H // 256) ** 2  # 53.97 at 512x512 (§8(d)); conv1 scales the same
-    extra = {"conv_whole_step": {"gflop_per_image": gflop_img,
-                                 "achieved": value * gflop_img / 1e3, "peak": PEAK_BF16_TFLOPS,
-                                 "unit": "TFLOP/s",
-                                 "frac": value * gflop_img / 1e3 / PEAK_BF16_TFLOPS}}
-    if loss_ms:
-        tps = B * R ** 3 * LOSS_TRANSC_PER_VOXEL / (loss_ms * 1e-3) / 1e12
-        extra["implicit_loss"] = {"call_ms_graph": loss_ms, "achieved": tps, "peak": PEAK_TRANSC_TPS,
-                                  "unit": "T transcendentals/s", "frac": tps / PEAK_TRANSC_TPS,
-                                  "hbm_bytes_per_image": R * R * 4 + 96}
-    tr = load_traffic()
-    if tr and tr.get("kernel_key") == list(PROBE) and H == 256:
-        roof["traffic"] = tr.get("hbm_bytes_per_launch")
+    dname = {torch.bfloat16: "bf16", torch.float16: "fp16"}[tr.dtype]
 
     workload = {2: "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
+                3: "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam, data parallel" % R,
                 4: "ResNetSQ + ExplicitLoss(R=32)(labels) + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
-                5: "ResNetSQ at 512x512 + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam (bf16: no loss "
-                   "scaling needed; the fp16 variant of config 5 is not built)" % R}[args.config]
-    out = {"metric": "training images/sec (%dx%d depth, %s loss)" % (H, H, "explicit+implicit" if crit_x else "implicit"),
+                5: "ResNetSQ at 512x512 + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam, %s%s"
+                   % (R, dname, " + dynamic loss scaling" if tr.scaler is not None else "")}[args.config]
+    out = {"metric": "training images/sec (%dx%d depth, %s loss)" % (H, H, "explicit+implicit" if tr.crit_x else "implicit"),
            "value": value, "unit": "images/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
            "data": "synthetic (GPU-rendered SQ depth images, reference label distribution)",
            "config": {"workload": workload, "baseline_config": args.config,
                       "model": "ResNetSQ (resnet18 backbone, 11.37M params)", "global_batch": B * world,
                       "per_gpu_batch": B, "image": "%dx%dx1" % (H, H), "render_size": R,
                       "parallelism": "dp%d" % world},
-           "mean_loss": mean_loss, "hip_graph": use_graph,
-           "dp": ("graph-captured RCCL all-reduce" if gdp is not None else ("DDP" if world > 1 else None)),
-           "roofline": roof, "roofline_extra": extra}
+           "final_loss": final_loss, "hip_graph": tr.use_graph,
+           "dp": ("graph-captured RCCL all-reduce" if tr.gdp is not None else ("DDP" if world > 1 else None))}
+    if tr.dp_note:
+        out["dp_note"] = tr.dp_note
+    if tr.scaler is not None:
+        out["loss_scale"] = float(tr.scaler.get_scale())
 
-    if rank == 0 and world == 1 and args.cpu_steps > 0 and args.config == 2:
-        imgs_cpu = images.detach().cpu()
-        v, secs = cpu_baseline(imgs_cpu, state0, R, args.cpu_steps)
-        out["cpu_baseline"] = {"value": v, "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": "%d train steps (1 warm-up) of batch %d: oracle/ref_torch.py ResNetSQ "
-                                         "fp32 + reference-style f64 ImplicitLoss(R=%d), Adam; %.1f s"
-                                         % (args.cpu_steps, B, R, secs)}
+    if not args.profile:
+        kern_ms, nlaunch, how = time_probe(tr)
+        flops = tr.probe_flops()
+        achieved = flops / (kern_ms * 1e-3) / 1e12 if nlaunch else None
+        ph = tr.probe_key()[3]
+        roof = {"bound": "mfma", "kernel": "conv_%s %dx%d 3x3 s1 64->64 (layer1 %s direct conv, %s)"
+                                           % (PROBE[0], ph, ph, "persistent" if ph == 64 else "tiled", dname),
+                "achieved": achieved, "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": (achieved / PEAK_MFMA_TFLOPS) if achieved else None,
+                "kernel_ms": kern_ms, "launches": nlaunch, "timing": how,
+                "flop_per_launch": flops, "traffic": None}
+        path = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                trf = json.load(f)
+            if trf.get("kernel_key") == list(PROBE) and H == 256 and dname == "bf16":
+                roof["traffic"] = trf.get("hbm_bytes_per_launch")
+        out["roofline"] = roof
+        # secondary rooflines: the whole step's conv work against the MFMA peak, and
+        # the fused loss call against the transcendental rate (per voxel ~21 exp2/log2/rcp, fwd + bwd)
+        gflop_img = CONV_GFLOP_PER_IMG * (H // 256) ** 2  # 53.97 at 512x512 (§8(d))
+        extra = {"conv_whole_step": {"gflop_per_image": gflop_img, "achieved": value / world * gflop_img / 1e3,
+                                     "peak": PEAK_MFMA_TFLOPS, "unit": "TFLOP/s",
+                                     "frac": value / world * gflop_img / 1e3 / PEAK_MFMA_TFLOPS}}
+        loss_ms = time_loss_call(tr.crit, tr.images, B, dev) if rank == 0 else None
+        if loss_ms:
+            tps = B * R ** 3 * LOSS_TRANSC_PER_VOXEL / (loss_ms * 1e-3) / 1e12
+            extra["implicit_loss"] = {"call_ms_graph": loss_ms, "achieved": tps, "peak": PEAK_TRANSC_TPS,
+                                      "unit": "T transcendentals/s", "frac": tps / PEAK_TRANSC_TPS,
+                                      "hbm_bytes_per_image": R * R * 4 + 96}
+        out["roofline_extra"] = extra
+        if rank == 0 and world == 1 and args.cpu_steps > 0 and args.config == 2:
+            out["cpu_baseline"] = cpu_baseline(tr.images.detach().cpu(), tr.params.detach().cpu(), tr.state0, R,
+                                               args.cpu_steps, args.cpu1_steps)
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     dist.finish()

@@ -27,6 +27,8 @@
  *   sqr_stem_fwd / _bwd        resnet18 stem bn1 -> relu -> maxpool(3,2,1) (torch/models.py:181).
  *   sqr_stem_fused_fwd / _bwd  the same stem + conv1 (torch/models.py:181-184) in one pass, bf16.
  *   sqr_adam_step              torch.optim.Adam step of torch/train.py:50-54 (+ conv weight packing).
+ *   sqr_amp_*, sqr_adam_step_amp  torch.amp.GradScaler around that step (fp16 config 5; the reference
+ *                              trains fp32 and has no scaler — this is the scaler torch pairs with fp16).
  *   sqr_tail_fwd / _bwd        ResNetSQ avgpool + encoder.fc + output heads (torch/models.py:7-99,186-204).
  */
 #ifndef SQR_H
@@ -48,6 +50,7 @@ extern "C" {
 /* element types for the conv entry points */
 #define SQR_DTYPE_F32 0
 #define SQR_DTYPE_BF16 1
+#define SQR_DTYPE_F16 2 /* IEEE half (BASELINE config 5: fp16 + dynamic loss scaling) */
 
 int sqr_version(void);
 const char* sqr_last_error_string(void);
@@ -57,6 +60,16 @@ const char* sqr_last_error_string(void);
  * kernel of a sqr_conv2d_* call, not its im2col / split-K reduction launches); the hook then
  * disarms itself.  NULL, NULL disarms.  Per calling thread. */
 int sqr_probe_arm(void* start_event, void* stop_event);
+/* Clock probe (bench.py's roofline timing inside the replayed step graph, where events cannot
+ * bracket one kernel node): the NEXT main conv kernel launched by this thread (then the hook
+ * disarms) records, into the device slots[0] / slots[1] (u64; the caller sets them to UINT64_MAX / 0
+ * before the kernel runs), the wall clock of its first workgroup's start (atomic min) and of its last
+ * workgroup's end after its stores drained (atomic max).  Kernel node parameters are fixed at graph
+ * capture, so every replay of a captured launch records into the same slots.  Supported by the
+ * direct 3x3 kernels (the others ignore it).  slots = NULL disarms. */
+int sqr_probe_arm_clock(unsigned long long* slots);
+/* ticks per millisecond of that clock (hipDeviceAttributeWallClockRate) */
+int sqr_wall_clock_khz(int* khz);
 
 /* ---------------------------------------------------------------- losses */
 
@@ -89,12 +102,16 @@ int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pred, int B, i
  * computed in float64 like the reference. */
 int sqr_iou_counts(const float* p_true, const float* p_pred, int B, int R, long long* counts,
                    void* stream);
+/* the same for float64 parameters (torch/visu.py:142-159 feeds f64 params; no rounding to f32) */
+int sqr_iou_counts_f64(const double* p_true, const double* p_pred, int B, int R, long long* counts,
+                       void* stream);
 
 /* ---------------------------------------------------------------- conv2d (implicit GEMM, NHWC) */
 
 /* Activations are NHWC (torch channels_last), weights KRSC for fwd/wgrad and CRSK for dgrad
  * (sqr_conv2d_pack_weight produces both from torch's KCRS fp32 master weight).
- * dtype SQR_DTYPE_BF16: bf16 in/out, fp32 accumulation (MFMA 16x16x32 bf16).
+ * dtype SQR_DTYPE_BF16: bf16 in/out, fp32 accumulation (MFMA 16x16x32 / 32x32x16 bf16).
+ * dtype SQR_DTYPE_F16 : fp16 in/out, fp32 accumulation (MFMA 16x16x32 / 32x32x16 f16), same kernels.
  * dtype SQR_DTYPE_F32 : f32 in/out, exact-f32 MFMA (16x16x4 f32) — the parity mode. */
 typedef struct sqr_conv_desc {
   int N, C, H, W;   /* input */
@@ -242,6 +259,22 @@ typedef struct sqr_adam_param {
 } sqr_adam_param;
 int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2, double eps,
                   double grad_scale, void* stream);
+
+/* ---------------------------------------------------------------- dynamic loss scaling (fp16)
+ * torch.amp.GradScaler (init_scale 2^16, growth 2, backoff 0.5, interval 2000) as three stream-ordered,
+ * graph-capturable device steps around a backward of `loss * (*loss_scale)`:
+ *   sqr_amp_check_finite  found_inf |= any non-finite element in the gradients (host arrays of device
+ *                         pointers / sizes; *found_inf must be 0 before the first call of a step);
+ *   sqr_adam_step_amp     sqr_adam_step on gradients g / (*loss_scale) that does nothing at all (no
+ *                         update, no step-counter increment, no packing) when *found_inf != 0;
+ *   sqr_amp_update_scale  GradScaler.update(): *found_inf ? scale *= backoff, tracker = 0
+ *                         : ++tracker == interval ? scale *= growth, tracker = 0; then *found_inf = 0.
+ * loss_scale f32, found_inf / growth_tracker int32, all device pointers. */
+int sqr_amp_check_finite(const float* const* grads, const long long* sizes, int n, int* found_inf, void* stream);
+int sqr_adam_step_amp(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2, double eps,
+                      double grad_scale, const float* loss_scale, const int* found_inf, void* stream);
+int sqr_amp_update_scale(float* loss_scale, int* growth_tracker, int* found_inf, float growth_factor,
+                         float backoff_factor, int growth_interval, void* stream);
 
 /* ---------------------------------------------------------------- ResNetSQ tail (fused) */
 

@@ -144,11 +144,12 @@ class ResNetSQRef(nn.Module):
                 torch.sigmoid(self.output_position.out_layer(f)), q / torch.norm(q, 2, -1, keepdim=True))
 
 
-def train_step(net, opt, loss_fn, images):
-    """torch/train.py:86-103 on CPU: zero_grad, forward, cat, loss(image, pred), backward, step."""
+def train_step(net, opt, loss_fn, images, labels=None):
+    """torch/train.py:86-103 on CPU: zero_grad, forward, cat, loss(image, pred), backward, step.
+    With labels given the loss is loss_fn(labels, pred) (ExplicitLoss, train.py:62-63)."""
     opt.zero_grad()
     pred = torch.cat(net(images), dim=1)
-    loss = loss_fn(images, pred)
+    loss = loss_fn(images if labels is None else labels, pred)
     loss.backward()
     opt.step()
     return loss.item()

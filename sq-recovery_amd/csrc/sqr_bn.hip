@@ -3,7 +3,7 @@
 // conv-bn, +identity, relu), forward (training batch statistics / eval running statistics) and
 // backward.  These are the memory-bound glue between the implicit-GEMM convs.
 //
-// Layout: activations [M pixels][C] (NHWC), bf16 or f32; BN parameters/statistics f32.
+// Layout: activations [M pixels][C] (NHWC), bf16, fp16 or f32; BN parameters/statistics f32.
 // Per-channel reductions are two-stage and deterministic: blocks accumulate float64 partial sums
 // over fixed pixel ranges (16-B vector loads, 8 channels per thread), a finalize kernel adds the
 // per-block partials in block order.  Elementwise passes are one read + one write per tensor.
@@ -17,6 +17,7 @@ namespace sqr {
 namespace bn {
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -37,6 +38,21 @@ template <> struct V8<bf16> {
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
     *(bf16x8*)p = o;
+  }
+};
+template <> struct V8<f16> {
+  static __device__ __forceinline__ void load(const f16* p, float* v) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    const f16x8 u = *(const f16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)u[i];
+  }
+  static __device__ __forceinline__ void store(f16* p, const float* v) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    f16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (f16)v[i];
+    *(f16x8*)p = o;
   }
 };
 template <> struct V8<float> {
@@ -337,7 +353,7 @@ __global__ void __launch_bounds__(256) bnrelu_maxpool_fwd_kernel(const T* __rest
         for (int k = 0; k < 8; ++k) {
           // relu output rounded to the activation dtype, as the unfused path stores it
           float t = fmaxf(fmaf(xv[k], sc[k], sh[k]), 0.f);
-          if (sizeof(T) == 2) t = (float)(bf16)t;
+          if (sizeof(T) == 2) t = (float)(T)t;
           if (t > best[k]) {
             best[k] = t;
             bi[k] = (uint8_t)(dh * 3 + dw);
@@ -555,7 +571,7 @@ int check_mc(long long M, int C, int dtype) {
                 "bn: C=%d must be a multiple of 8 with C/8 dividing 256", C);
   SQR_CHECK_ARG(C / 8 <= 256 && ((C / 8) & (C / 8 - 1)) == 0, "bn: C=%d must be 8 * a power of two <= 2048", C);
   SQR_CHECK_ARG(M * (C / 8) < (1ll << 31), "bn: tensor too large");
-  SQR_CHECK_ARG(dtype == SQR_DTYPE_F32 || dtype == SQR_DTYPE_BF16, "bn: bad dtype");
+  SQR_CHECK_ARG(dtype == SQR_DTYPE_F32 || dtype == SQR_DTYPE_BF16 || dtype == SQR_DTYPE_F16, "bn: bad dtype");
   return 0;
 }
 
@@ -619,6 +635,9 @@ extern "C" int sqr_bn_fwd(const void* x, long long M, int C, int dtype, const fl
   if (dtype == SQR_DTYPE_BF16)
     return bn_fwd_impl<bf16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training,
                              residual, relu, y, relu_mask, save_mean, save_invstd, workspace, st);
+  if (dtype == SQR_DTYPE_F16)
+    return bn_fwd_impl<f16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training,
+                             residual, relu, y, relu_mask, save_mean, save_invstd, workspace, st);
   return bn_fwd_impl<float>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, training, residual,
                             relu, y, relu_mask, save_mean, save_invstd, workspace, st);
 }
@@ -656,6 +675,9 @@ extern "C" int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* 
   hipStream_t st = as_stream(stream);
   if (dtype == SQR_DTYPE_BF16)
     return bn_bwd_impl<bf16>(dy, relu_mask, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta,
+                             workspace, st);
+  if (dtype == SQR_DTYPE_F16)
+    return bn_bwd_impl<f16>(dy, relu_mask, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta,
                              workspace, st);
   return bn_bwd_impl<float>(dy, relu_mask, x, (int)M, C, gamma, save_mean, save_invstd, dx, dres, dgamma, dbeta,
                             workspace, st);
@@ -716,6 +738,9 @@ extern "C" int sqr_stem_fwd(const void* x, int N, int H, int W, int C, int dtype
   if (dtype == SQR_DTYPE_BF16)
     return stem_fwd_impl<bf16>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, training, y,
                                argmax, save_mean, save_invstd, workspace, st);
+  if (dtype == SQR_DTYPE_F16)
+    return stem_fwd_impl<f16>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, training, y,
+                               argmax, save_mean, save_invstd, workspace, st);
   return stem_fwd_impl<float>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, training, y,
                               argmax, save_mean, save_invstd, workspace, st);
 }
@@ -763,6 +788,9 @@ extern "C" int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t*
   if (dtype == SQR_DTYPE_BF16)
     return stem_bwd_impl<bf16>(dpool, ypool, argmax, x, N, H, W, C, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
                                workspace, st);
+  if (dtype == SQR_DTYPE_F16)
+    return stem_bwd_impl<f16>(dpool, ypool, argmax, x, N, H, W, C, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
+                               workspace, st);
   return stem_bwd_impl<float>(dpool, ypool, argmax, x, N, H, W, C, gamma, save_mean, save_invstd, dx, dgamma, dbeta,
                               workspace, st);
 }
@@ -784,6 +812,9 @@ extern "C" int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, co
   if (dtype == SQR_DTYPE_BF16)
     return bn_fwd_impl<bf16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
                              relu_mask, save_mean, save_invstd, workspace, st, stats, stats_rows);
+  if (dtype == SQR_DTYPE_F16)
+    return bn_fwd_impl<f16>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
+                             relu_mask, save_mean, save_invstd, workspace, st, stats, stats_rows);
   return bn_fwd_impl<float>(x, (int)M, C, gamma, beta, running_mean, running_var, momentum, eps, 1, residual, relu, y,
                             relu_mask, save_mean, save_invstd, workspace, st, stats, stats_rows);
 }
@@ -804,6 +835,9 @@ extern "C" int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int
   hipStream_t st = as_stream(stream);
   if (dtype == SQR_DTYPE_BF16)
     return stem_fwd_impl<bf16>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, 1, y, argmax,
+                               save_mean, save_invstd, workspace, st, stats, stats_rows);
+  if (dtype == SQR_DTYPE_F16)
+    return stem_fwd_impl<f16>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, 1, y, argmax,
                                save_mean, save_invstd, workspace, st, stats, stats_rows);
   return stem_fwd_impl<float>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, 1, y, argmax,
                               save_mean, save_invstd, workspace, st, stats, stats_rows);

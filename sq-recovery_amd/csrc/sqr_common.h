@@ -12,6 +12,9 @@ void set_error(const char* fmt, ...);
 // sqr_probe_arm: record the armed events around the next main conv kernel launch (then disarm)
 void probe_begin(hipStream_t st);
 void probe_end(hipStream_t st);
+// sqr_probe_arm_clock: the device slot pair the next main conv kernel launch records its wall-clock
+// span into (one-shot: returns nullptr when not armed, disarms otherwise)
+unsigned long long* probe_clock_take();
 
 #define SQR_CHECK_ARG(cond, ...)            \
   do {                                      \

@@ -20,7 +20,7 @@
 //       reduce kernel sums in a fixed order (bitwise reproducible) while permuting to torch's
 //       [K][C][R][S] weight-grad layout.
 //
-// MFMA: bf16 -> v_mfma_f32_16x16x32_bf16; f32 (parity mode) -> v_mfma_f32_16x16x4_f32 (exact
+// MFMA: bf16 / fp16 -> v_mfma_f32_16x16x32_{bf16,f16}; f32 (parity mode) -> v_mfma_f32_16x16x4_f32 (exact
 // f32 products, f32 accumulation).  The MFMA A operand is always the output's contiguous
 // dimension, so each lane owns 4 consecutive output channels of one pixel and stores them with
 // one 8-B (bf16) / 16-B (f32) store — no LDS epilogue.
@@ -213,17 +213,17 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
 #pragma unroll
     for (int sub = 0; sub < BK / C::KSUB; ++sub) {
       if constexpr (C::ES == 2) {
-        bf16x8 pf[TN], qf[TM];
+        V8<T> pf[TN], qf[TM];
         const int slot = 4 * sub + fq;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int row = wn * WN + 16 * j + fr;
-          pf[j] = *(const bf16x8*)(p + row * ROWB + nt_swz(row, slot) * 16);
+          pf[j] = *(const V8<T>*)(p + row * ROWB + nt_swz(row, slot) * 16);
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int row = wm * WM + 16 * i + fr;
-          qf[i] = *(const bf16x8*)(q + row * ROWB + nt_swz(row, slot) * 16);
+          qf[i] = *(const V8<T>*)(q + row * ROWB + nt_swz(row, slot) * 16);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 #pragma unroll
     for (int sub = 0; sub < BK / C::KSUB; ++sub) {
       if constexpr (C::ES == 2) {
-        bf16x8 pf[TN], qf[TM];
+        V8<T> pf[TN], qf[TM];
         s16x4 plo[TN], phi[TN], qlo[TM], qhi[TM];
         // lane (fq, fr): rows k = 32 sub + 8 fq + (fr>>2) (+4), cols c0 + 4 (fr&3)
         const int krow = 32 * sub + 8 * fq + (fr >> 2);
@@ -500,12 +500,12 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const s16x8 v = {plo[j][0], plo[j][1], plo[j][2], plo[j][3], phi[j][0], phi[j][1], phi[j][2], phi[j][3]};
-          pf[j] = __builtin_bit_cast(bf16x8, v);
+          pf[j] = __builtin_bit_cast(V8<T>, v);
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const s16x8 v = {qlo[i][0], qlo[i][1], qlo[i][2], qlo[i][3], qhi[i][0], qhi[i][1], qhi[i][2], qhi[i][3]};
-          qf[i] = __builtin_bit_cast(bf16x8, v);
+          qf[i] = __builtin_bit_cast(V8<T>, v);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -797,10 +797,12 @@ __global__ void __launch_bounds__(256) pack_weights_batched_kernel(PackJobs jobs
   if (blockIdx.z == 0) {
     if (!jb.krsc || row >= jb.K) return;
     if (jb.dtype == SQR_DTYPE_BF16) pack_krsc_row<bf16>(jb, row, plds);
+    else if (jb.dtype == SQR_DTYPE_F16) pack_krsc_row<f16>(jb, row, plds);
     else pack_krsc_row<float>(jb, row, plds);
   } else {
     if (!jb.crsk || row >= jb.C) return;
     if (jb.dtype == SQR_DTYPE_BF16) pack_crsk_row<bf16>(jb, row, plds);
+    else if (jb.dtype == SQR_DTYPE_F16) pack_crsk_row<f16>(jb, row, plds);
     else pack_crsk_row<float>(jb, row, plds);
   }
 }
@@ -833,8 +835,9 @@ int check_desc(const sqr_conv_desc* d, Shape* sh) {
   SQR_CHECK_ARG(d->N >= 1 && d->C >= 1 && d->H >= 1 && d->W >= 1 && d->K >= 1 && d->R >= 1 && d->S >= 1,
                 "conv2d: non-positive dims");
   SQR_CHECK_ARG(d->stride >= 1 && d->pad >= 0, "conv2d: bad stride/pad");
-  SQR_CHECK_ARG(d->dtype == SQR_DTYPE_F32 || d->dtype == SQR_DTYPE_BF16, "conv2d: bad dtype %d", d->dtype);
-  sh->ES = d->dtype == SQR_DTYPE_BF16 ? 2 : 4;
+  SQR_CHECK_ARG(d->dtype == SQR_DTYPE_F32 || d->dtype == SQR_DTYPE_BF16 || d->dtype == SQR_DTYPE_F16,
+                "conv2d: bad dtype %d", d->dtype);
+  sh->ES = d->dtype == SQR_DTYPE_F32 ? 4 : 2;
   sh->Ho = (d->H + 2 * d->pad - d->R) / d->stride + 1;
   sh->Wo = (d->W + 2 * d->pad - d->S) / d->stride + 1;
   SQR_CHECK_ARG(sh->Ho >= 1 && sh->Wo >= 1, "conv2d: empty output");
@@ -842,13 +845,15 @@ int check_desc(const sqr_conv_desc* d, Shape* sh) {
   const long long Min = (long long)d->N * d->H * d->W;
   SQR_CHECK_ARG(M < (1ll << 31) && Min < (1ll << 31), "conv2d: too many pixels");
   SQR_CHECK_ARG(d->C >= 8 || M * 64 < (1ll << 31), "conv2d: too many pixels for the im2col path");
-  // 32-bit buffer offsets: every operand tensor must stay below 2 GiB
-  SQR_CHECK_ARG(Min * d->C * 4 < (1ll << 31) && M * d->K * 4 < (1ll << 31) && M * 512 * 4 < (1ll << 32),
-                "conv2d: tensors larger than 2 GiB are not supported");
   sh->M = (int)M;
   sh->im2col = d->C < 8;
   sh->Kp = 64;  // im2col K: next power of two >= max(64, R*S*C) (the gather needs a power-of-2 row)
   while (sh->Kp < d->R * d->S * d->C) sh->Kp *= 2;
+  // 32-bit buffer offsets: every operand tensor (and the im2col matrix) must stay below 2 GiB
+  const long long es = d->dtype == SQR_DTYPE_F32 ? 4 : 2;
+  SQR_CHECK_ARG(Min * d->C * es < (1ll << 31) && M * d->K * es < (1ll << 31) &&
+                    (!sh->im2col || M * sh->Kp * es < (1ll << 31)),
+                "conv2d: tensors larger than 2 GiB are not supported");
   const int vec = 16 / sh->ES;
   SQR_CHECK_ARG(sh->im2col || (is_pow2(d->C) && d->C % vec == 0), "conv2d: C=%d must be a power of 2 >= 8", d->C);
   SQR_CHECK_ARG(d->K % 8 == 0 && is_pow2(d->K), "conv2d: K=%d must be a power of 2 >= 8", d->K);
@@ -1018,9 +1023,9 @@ extern "C" int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo) {
   return 0;
 }
 
-// bf16 3x3 / stride 1 / pad 1 (the direct kernels' domain; they decline other shapes themselves)
+// 16-bit 3x3 / stride 1 / pad 1 (the direct kernels' domain; they decline other shapes themselves)
 static bool direct3(const sqr_conv_desc* d, const Shape& sh) {
-  return !sh.im2col && d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1;
+  return !sh.im2col && d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1;
 }
 
 extern "C" size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which) {
@@ -1049,9 +1054,10 @@ extern "C" int sqr_conv2d_pack_weight(const float* w_kcrs, const sqr_conv_desc* 
   const int total = d->K * (sh.im2col ? sh.Kp : d->R * d->S * d->C);
   const int blocks = (total + 255) / 256;
   hipStream_t st = as_stream(stream);
-  if (d->dtype == SQR_DTYPE_BF16)
-    hipLaunchKernelGGL((pack_weight_kernel<bf16>), dim3(blocks), dim3(256), 0, st, w_kcrs, d->K, d->C, d->R, d->S,
-                       d->stride, d->pad, (int)sh.im2col, sh.Kp, (bf16*)w_krsc, (bf16*)w_crsk);
+  if (d->dtype != SQR_DTYPE_F32)
+    SQR_DISPATCH16(d->dtype, T,
+                   hipLaunchKernelGGL((pack_weight_kernel<T>), dim3(blocks), dim3(256), 0, st, w_kcrs, d->K, d->C,
+                                      d->R, d->S, d->stride, d->pad, (int)sh.im2col, sh.Kp, (T*)w_krsc, (T*)w_crsk));
   else
     hipLaunchKernelGGL((pack_weight_kernel<float>), dim3(blocks), dim3(256), 0, st, w_kcrs, d->K, d->C, d->R,
                        d->S, d->stride, d->pad, (int)sh.im2col, sh.Kp, (float*)w_krsc, (float*)w_crsk);
@@ -1084,13 +1090,13 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
   a.oph = a.opw = 0;
   a.oH = sh.Ho;
   a.oW = sh.Wo;
-  if (!sh.im2col && d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1) {
-    rc = conv3_launch(x, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, st);
-    if (rc != 1) return rc;  // launched (0) or failed; 1 = shape not covered by the direct kernel
+  if (direct3(d, sh)) {
+    rc = conv3_launch(d->dtype, x, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, st);
+    if (rc != kNotHandled) return rc;  // launched (0) or failed; else the shape is not covered
   }
   a.stats = stats;
   if (stats_rows) {  // one partial row per M tile of the config launch_nt will pick
-    const int bm = kNtBM[nt_pick(sh.M, d->K, d->dtype == SQR_DTYPE_BF16)];
+    const int bm = kNtBM[nt_pick(sh.M, d->K, d->dtype != SQR_DTYPE_F32)];
     *stats_rows = (sh.M + bm - 1) / bm;
   }
   if (sh.im2col) {
@@ -1099,7 +1105,8 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
       set_error("conv2d_fwd: workspace %zu < %zu", workspace_bytes, need);
       return SQR_E_WORKSPACE;
     }
-    rc = d->dtype == SQR_DTYPE_BF16 ? im2col<bf16>(x, d, sh, workspace, st) : im2col<float>(x, d, sh, workspace, st);
+    if (d->dtype == SQR_DTYPE_F32) rc = im2col<float>(x, d, sh, workspace, st);
+    else SQR_DISPATCH16(d->dtype, T, rc = im2col<T>(x, d, sh, workspace, st));
     if (rc) return rc;
     a.g = make_gather(workspace, sh.Ho, sh.Wo, sh.Kp, sh.Ho, sh.Wo, 1, 0, 0, 1, 1, 1, d->N, sh.ES);
     a.Kg = sh.Kp;
@@ -1107,7 +1114,9 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
     a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, -d->pad, 1, d->R, d->S, d->N, sh.ES);
     a.Kg = d->R * d->S * d->C;
   }
-  return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(&a, 1, st) : launch_nt<float>(&a, 1, st);
+  if (d->dtype == SQR_DTYPE_F32) return launch_nt<float>(&a, 1, st);
+  SQR_DISPATCH16(d->dtype, T, rc = launch_nt<T>(&a, 1, st));
+  return rc;
 }
 
 extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d,
@@ -1155,15 +1164,15 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
   SQR_CHECK_ARG(!sh.im2col, "conv2d_bwd_data: C=%d < 8 not supported", d->C);
   SQR_CHECK_ARG(dy && w_crsk && dx, "conv2d_bwd_data: null pointer");
   hipStream_t st = as_stream(stream);
-  if (d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1) {
-    rc = conv3_launch(dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, st);
-    if (rc != 1) return rc;
+  if (direct3(d, sh)) {
+    rc = conv3_launch(d->dtype, dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, st);
+    if (rc != kNotHandled) return rc;
   }
-  if (d->dtype == SQR_DTYPE_BF16 && d->R == 3 && d->S == 3 && d->stride == 2 && d->pad == 1 &&
+  if (d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->stride == 2 && d->pad == 1 &&
       d->H == 2 * sh.Ho && d->W == 2 * sh.Wo) {
     const int off[4] = {0, d->C * d->K, 3 * d->C * d->K, 5 * d->C * d->K};  // classes of 1, 2, 2, 4 taps
-    rc = conv3s2_dgrad_launch(dy, w_crsk, off, dx, d->N, sh.Ho, sh.Wo, d->K, d->C, st);
-    if (rc != 1) return rc;
+    rc = conv3s2_dgrad_launch(d->dtype, dy, w_crsk, off, dx, d->N, sh.Ho, sh.Wo, d->K, d->C, st);
+    if (rc != kNotHandled) return rc;
   }
   // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+p-r)/st,(w+p-s)/st,k] W[k,c,r,s] over the divisible taps.
   // Output pixels split by parity (h%st, w%st); in class (ph,pw) only taps r = r0 + st*t contribute
@@ -1193,7 +1202,9 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
     }
   }
   if (ncls == 0) return 0;
-  return d->dtype == SQR_DTYPE_BF16 ? launch_nt<bf16>(cl, ncls, st) : launch_nt<float>(cl, ncls, st);
+  if (d->dtype == SQR_DTYPE_F32) return launch_nt<float>(cl, ncls, st);
+  SQR_DISPATCH16(d->dtype, T, rc = launch_nt<T>(cl, ncls, st));
+  return rc;
 }
 
 static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, float* dw_kcrs,
@@ -1216,7 +1227,8 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   if (sh.im2col) {
     const void* col = col_in;
     if (!col) {
-      rc = d->dtype == SQR_DTYPE_BF16 ? im2col<bf16>(x, d, sh, ws, st) : im2col<float>(x, d, sh, ws, st);
+      if (d->dtype == SQR_DTYPE_F32) rc = im2col<float>(x, d, sh, ws, st);
+      else SQR_DISPATCH16(d->dtype, T, rc = im2col<T>(x, d, sh, ws, st));
       if (rc) return rc;
       col = ws;
       ws += colb;
@@ -1230,13 +1242,13 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   if (direct3(d, sh)) {
     int splits = 0;
     const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
-    rc = conv3w_launch(x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
+    rc = conv3w_launch(d->dtype, x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
     if (rc == 0) {
       rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st);
       if (rc) return rc;
       return 0;
     }
-    if (rc != 1) return rc;
+    if (rc != kNotHandled) return rc;
   }
   a.dy = dy;
   a.Kout = d->K;
@@ -1249,7 +1261,8 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
     else if (BK % Wo == 0 && Ho % (BK / Wo) == 0) a.rect_wt = Wo;
   }
   const TNPlan p = plan_tn(d->K, Ng, sh.M, sh.ES);
-  rc = d->dtype == SQR_DTYPE_BF16 ? launch_tn<bf16>(a, p, st) : launch_tn<float>(a, p, st);
+  if (d->dtype == SQR_DTYPE_F32) rc = launch_tn<float>(a, p, st);
+  else SQR_DISPATCH16(d->dtype, T, rc = launch_tn<T>(a, p, st));
   if (rc) return rc;
   return launch_wgrad_reduce((const float*)ws, p.splits, d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C,
                              (int)sh.im2col, dw_kcrs, st);
@@ -1277,7 +1290,8 @@ extern "C" int sqr_conv2d_pack_weights(const sqr_pack_job* jobs, int njobs, void
     SQR_CHECK_ARG(d->K >= 1 && d->C >= 1 && d->R >= 1 && d->S >= 1 && d->stride >= 1 && d->stride <= 2 &&
                       d->pad >= 0,
                   "conv2d_pack_weights: job %d bad dims (stride <= 2)", i);
-    SQR_CHECK_ARG(d->dtype == SQR_DTYPE_F32 || d->dtype == SQR_DTYPE_BF16, "conv2d_pack_weights: bad dtype");
+    SQR_CHECK_ARG(d->dtype == SQR_DTYPE_F32 || d->dtype == SQR_DTYPE_BF16 || d->dtype == SQR_DTYPE_F16,
+                  "conv2d_pack_weights: bad dtype");
     const int im2col = d->C < 8;
     SQR_CHECK_ARG(!(im2col && jobs[i].w_crsk), "conv2d_pack_weights: no dgrad weights for C<8 convs");
     int kp = 64;

@@ -1,4 +1,4 @@
-// Direct 3x3 / stride 1 / pad 1 convolution (forward and backward-data), bf16, gfx950 MFMA.
+// Direct 3x3 / stride 1 / pad 1 convolution (forward and backward-data), bf16 / fp16, gfx950 MFMA.
 //
 // The generic implicit-GEMM kernel (sqr_conv.hip conv_nt_kernel) gathers every (pixel, tap) row
 // of the im2col matrix separately: per 64-channel k-tile it pays one LDS-DMA piece per 8 rows
@@ -33,8 +33,6 @@
 namespace sqr {
 namespace conv {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
 // 16-B slot XOR key of a 128-B LDS row (see the header): shift-invariant conflict-free b128 reads
 __device__ __forceinline__ int d3key(int row) { return row & 6; }
 
@@ -48,6 +46,7 @@ struct D3Args {
   int ntm, ntn;
   int flip;
   uint32_t xbytes, wbytes;
+  unsigned long long* tp;  // nullable: clock probe slots
 };
 
 // LDS-DMA issue of PIECES 1-KiB pieces per wave: piece i of wave w lands at rows
@@ -66,7 +65,7 @@ __device__ __forceinline__ void dma_pieces(__amdgpu_buffer_rsrc_t srd, char* dst
 // Per-lane sums over i (stats_accum), then an LDS transpose (stats_reduce): red[wave-row
 // group][fr][col] -> one thread per column adds its 16*WAVES_M partials in a fixed order
 // (deterministic, no cross-lane shuffles).
-template <int TM, int TN>
+template <typename T, int TM, int TN>
 __device__ __forceinline__ void stats_accum(const uint32_t (*pk)[TM][2], float (*s1)[4], float (*s2)[4]) {
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -74,7 +73,7 @@ __device__ __forceinline__ void stats_accum(const uint32_t (*pk)[TM][2], float (
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const float lo = __uint_as_float(pk[j][i][h] << 16), hi = __uint_as_float(pk[j][i][h] & 0xffff0000u);
+        const float lo = lo2f<T>(pk[j][i][h]), hi = hi2f<T>(pk[j][i][h]);
         s1[j][2 * h] += lo;
         s2[j][2 * h] = fmaf(lo, lo, s2[j][2 * h]);
         s1[j][2 * h + 1] += hi;
@@ -106,8 +105,8 @@ __device__ __forceinline__ void stats_reduce(const float (*s1)[4], const float (
 }
 
 // BatchNorm partials of a BM x BN output tile held as acc[j][i] (lane: pixel 16i+fr of its wave
-// rows, channels 16j+4fq..+3 of its wave columns), from the bf16 values actually stored.
-template <int BN, int WAVES_M, int WAVES_N, int TM, int TN, int NT>
+// rows, channels 16j+4fq..+3 of its wave columns), from the 16-bit values actually stored.
+template <typename T, int BN, int WAVES_M, int WAVES_N, int TM, int TN, int NT>
 __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* red, int wm, int wn, int fr, int fq,
                                            int tid, float* stats_row0, float* stats_row1) {
   float s1[TN][4], s2[TN][4];
@@ -115,7 +114,7 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
-  stats_accum<TM, TN>(pk, s1, s2);
+  stats_accum<T, TM, TN>(pk, s1, s2);
   stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(s1, s2, red, wm, wn, fr, fq, tid, stats_row0, stats_row1);
 }
 
@@ -123,7 +122,7 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 // (small late-layer images: more pixels per weight tile fetched)
 // PD: weight tiles prefetched ahead (ring of PD + 1 stages): the per-CU LDS-DMA delivery is
 // latency x bytes-in-flight bound, so deeper rings buy throughput where LDS allows
-template <int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2>
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
   constexpr int ROWB = 128, STAGES = PD + 1;
@@ -140,6 +139,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   static_assert(2 * WAVES_M * 16 * BN * 4 <= LDS, "stats scratch fits the ring");
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   char* const bring = smem + NWB * WIN;
+  clock_begin(a.tp);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -259,17 +259,17 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
-        bf16x8 pf[TN], qf[TM];
+        V8<T> pf[TN], qf[TM];
 #if SQR_EXP & 16
 #pragma unroll
-        for (int j = 0; j < TN; ++j) pf[j] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)poff[j], 0u, 0u, (uint32_t)sub});
+        for (int j = 0; j < TN; ++j) pf[j] = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)poff[j], 0u, 0u, (uint32_t)sub});
 #pragma unroll
-        for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)qoff[i], 0u, 0u, 0u});
+        for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)qoff[i], 0u, 0u, 0u});
 #else
 #pragma unroll
-        for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(bst + (poff[j] ^ (sub << 6)));
+        for (int j = 0; j < TN; ++j) pf[j] = *(const V8<T>*)(bst + (poff[j] ^ (sub << 6)));
 #pragma unroll
-        for (int i = 0; i < TM; ++i) qf[i] = *(const bf16x8*)(win + (qoff[i] ^ (sub << 6)));
+        for (int i = 0; i < TM; ++i) qf[i] = *(const V8<T>*)(win + (qoff[i] ^ (sub << 6)));
 #endif
 #if SQR_EXP & 8
 #pragma unroll
@@ -317,13 +317,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
-      const bf16x2 lo = {(bf16)acc[j][i][0], (bf16)acc[j][i][1]};
-      const bf16x2 hi = {(bf16)acc[j][i][2], (bf16)acc[j][i][3]};
-      pk[j][i][0] = __builtin_bit_cast(uint32_t, lo);
-      pk[j][i][1] = __builtin_bit_cast(uint32_t, hi);
+      pk[j][i][0] = pack2<T>(acc[j][i][0], acc[j][i][1]);
+      pk[j][i][1] = pack2<T>(acc[j][i][2], acc[j][i][3]);
     }
-  bf16* __restrict__ out = (bf16*)a.out;
+  uint16_t* __restrict__ out = (uint16_t*)a.out;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wm * WM + 16 * i + fr;
@@ -334,9 +331,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       *(u32x2*)(out + pix * a.Nout + n0 + wn * WN + 16 * j + 4 * fq) = u32x2{pk[j][i][0], pk[j][i][1]};
   }
   if (a.stats)
-    tile_stats<BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
+    tile_stats<T, BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
                                                  a.stats + ((size_t)tile_m * 2) * a.Nout + n0,
                                                  a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
+  clock_end(a.tp);
 }
 
 
@@ -357,6 +355,7 @@ struct D3PArgs {
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
   int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
+  unsigned long long* tp;  // nullable: clock probe slots
 };
 
 // s_waitcnt vmcnt(n) for the run-time n values the persistent kernel needs (wave-uniform)
@@ -373,6 +372,7 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
   // 2 x 2 waves, each 64 pixels (one image row) x 32 channels = two 32x32 MFMA accumulators
@@ -393,6 +393,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   char* const wl = smem;
   char* const ring = smem + WB;
   char* const stg = ring + RING;
+  clock_begin(a.tp);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -483,27 +484,27 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     // tap (r, c3) of output row hb+2k+wm reads input row hb+2k+wm+r-1 = ring slot (hb+2k+wm+r) & 7
     const int rbase = hb + 2 * k + wm;
     // 36 (tap, 16-channel slice) steps; slice kk of a 128-B row = 16-B slots 2kk + h
-    auto load = [&](int s, bf16x8& pf, bf16x8* qf) {
+    auto load = [&](int s, V8<T>& pf, V8<T>* qf) {
       const int t = s >> 2, kk = s & 3;
       const int r = t / 3, c3 = t % 3;
       const int rr = flip ? 2 - r : r, cc = flip ? 2 - c3 : c3;
       const int slot = 2 * kk + h;
       const int lrow0 = ((rbase + rr) & (NSLOT - 1)) * SLOTR + cc + r32;
 #if SQR_EXP & 1024
-      pf = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)(prow32 + slot), (uint32_t)t, 0u, 0u});
+      pf = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)(prow32 + slot), (uint32_t)t, 0u, 0u});
 #pragma unroll
-      for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(bf16x8, u32x4{(uint32_t)(lrow0 + i), 0u, 0u, 0u});
+      for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)(lrow0 + i), 0u, 0u, 0u});
 #else
-      pf = *(const bf16x8*)(wl + t * BN * ROWB + prow32 + ((slot ^ pkey) << 4));
+      pf = *(const V8<T>*)(wl + t * BN * ROWB + prow32 + ((slot ^ pkey) << 4));
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int L = lrow0 + 32 * i;
-        qf[i] = *(const bf16x8*)(ring + L * ROWB + ((slot ^ ((L >> 1) & 7)) << 4));
+        qf[i] = *(const V8<T>*)(ring + L * ROWB + ((slot ^ ((L >> 1) & 7)) << 4));
       }
 #endif
     };
     constexpr int NSTEP = 36, PD = 2;
-    bf16x8 pf[PD + 1], qf[PD + 1][TM];
+    V8<T> pf[PD + 1], qf[PD + 1][TM];
 #pragma unroll
     for (int s = 0; s < PD; ++s) load(s, pf[s], qf[s]);
 #if SQR_EXP & 128
@@ -514,7 +515,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       if (s + PD < NSTEP) load(s + PD, pf[(s + PD) % (PD + 1)], qf[(s + PD) % (PD + 1)]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[s % (PD + 1)], qf[s % (PD + 1)][i], acc[i], 0, 0, 0);
+        acc[i] = mfma32(pf[s % (PD + 1)], qf[s % (PD + 1)][i], acc[i]);
 #pragma unroll
       for (int g = 0; g < 1 + TM; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // a fragment read
@@ -529,14 +530,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        const bf16x2 lo = {(bf16)acc[i][4 * g], (bf16)acc[i][4 * g + 1]};
-        const bf16x2 hi = {(bf16)acc[i][4 * g + 2], (bf16)acc[i][4 * g + 3]};
-        pk[i][g][0] = __builtin_bit_cast(uint32_t, lo);
-        pk[i][g][1] = __builtin_bit_cast(uint32_t, hi);
+        pk[i][g][0] = pack2<T>(acc[i][4 * g], acc[i][4 * g + 1]);
+        pk[i][g][1] = pack2<T>(acc[i][4 * g + 2], acc[i][4 * g + 3]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          const float v0 = __uint_as_float(pk[i][g][q] << 16), v1 = __uint_as_float(pk[i][g][q] & 0xffff0000u);
+          const float v0 = lo2f<T>(pk[i][g][q]), v1 = hi2f<T>(pk[i][g][q]);
           st1[4 * g + 2 * q] += v0;
           st2[4 * g + 2 * q] = fmaf(v0, v0, st2[4 * g + 2 * q]);
           st1[4 * g + 2 * q + 1] += v1;
@@ -581,6 +579,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  clock_end(a.tp);
 }
 
 // ============================================================================ stride-2 dgrad
@@ -606,7 +605,7 @@ struct D3S2Args {
 
 __host__ __device__ constexpr int s2_ntaps(int cl) { return (1 + (cl >> 1)) * (1 + (cl & 1)); }
 
-template <int TH, int TW, int BN, int WAVES_M, int WAVES_N, int NCH, int PD>
+template <typename T, int TH, int TW, int BN, int WAVES_M, int WAVES_N, int NCH, int PD>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D3S2Args a) {
   constexpr int NW = WAVES_M * WAVES_N, ROWB = 128, STAGES = PD + 1;
   constexpr int BM = TH * TW, WM = BM / WAVES_M, WN = BN / WAVES_N, TM = WM / 16, TN = WN / 16;
@@ -725,11 +724,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
         }
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
-          bf16x8 pf[TN], qf[TM];
+          V8<T> pf[TN], qf[TM];
 #pragma unroll
-          for (int j = 0; j < TN; ++j) pf[j] = *(const bf16x8*)(bst + (poff[j] ^ (sub << 6)));
+          for (int j = 0; j < TN; ++j) pf[j] = *(const V8<T>*)(bst + (poff[j] ^ (sub << 6)));
 #pragma unroll
-          for (int i = 0; i < TM; ++i) qf[i] = *(const bf16x8*)(win + (qoff[i] ^ (sub << 6)));
+          for (int i = 0; i < TM; ++i) qf[i] = *(const V8<T>*)(win + (qoff[i] ^ (sub << 6)));
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -763,7 +762,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   }
   static_assert(SL >= 8, "staging swizzle assumes at least 8 slots per pixel");
   const int H = 2 * a.Ho, W = 2 * a.Wo;
-  bf16* __restrict__ out = (bf16*)a.dx;
+  T* __restrict__ out = (T*)a.dx;
 #pragma unroll
   for (int ph = 0; ph < 2; ++ph) {
     if (ph) __syncthreads();  // previous half copied out
@@ -780,7 +779,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
 #if SQR_EXP & 2048
           if (acc[2 * ph + pw][j][i][0] == 1.2345f)
 #endif
-          store4((bf16*)(smem + p * (BN * 2) + slot * 16 + (n & 4) * 2), acc[2 * ph + pw][j][i]);
+          store4((T*)(smem + p * (BN * 2) + slot * 16 + (n & 4) * 2), acc[2 * ph + pw][j][i]);
         }
       }
     __syncthreads();
@@ -832,7 +831,7 @@ struct D3WArgs {
   uint32_t xbytes, dybytes;
 };
 
-template <int TW, int TH, int STAGES>
+template <typename T, int TW, int TH, int STAGES>
 __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   constexpr int NW = 4, ROWB = 128;
   constexpr int BKP = TW * TH, SUBS = BKP / 32;      // pixels per chunk, 32-pixel k-steps
@@ -954,32 +953,32 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
           xb[h][c3] = xbase + xaddr[sub][h][c3];
           xb1[h][c3] = xb[h][c3] ^ 64u;
         }
-#define SQR_X_READ(T)                                                                                 \
+#define SQR_X_READ(TP)                                                                                 \
   do {                                                                                                \
-    constexpr int R_ = (T) / 3, S_ = (T) % 3, OFF_ = R_ * WWID * ROWB;                                \
-    xlo[T] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[0][S_] : xb[0][S_]);                                \
-    xhi[T] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[1][S_] : xb[1][S_]);                                \
+    constexpr int R_ = (TP) / 3, S_ = (TP) % 3, OFF_ = R_ * WWID * ROWB;                                \
+    xlo[TP] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[0][S_] : xb[0][S_]);                                \
+    xhi[TP] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[1][S_] : xb[1][S_]);                                \
   } while (0)
       SQR_X_READ(0);
       SQR_X_READ(1);
       asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 bfr[4];
+      V8<T> bfr[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const s16x8 v = {dlo[kt][0], dlo[kt][1], dlo[kt][2], dlo[kt][3], dhi[kt][0], dhi[kt][1], dhi[kt][2], dhi[kt][3]};
-        bfr[kt] = __builtin_bit_cast(bf16x8, v);
+        bfr[kt] = __builtin_bit_cast(V8<T>, v);
       }
-#define SQR_TAP(T)                                                                                     \
+#define SQR_TAP(TP)                                                                                     \
   do {                                                                                                 \
-    const s16x8 v_ = {xlo[T][0], xlo[T][1], xlo[T][2], xlo[T][3], xhi[T][0], xhi[T][1], xhi[T][2], xhi[T][3]}; \
-    const bf16x8 afr_ = __builtin_bit_cast(bf16x8, v_);                                                \
-    _Pragma("unroll") for (int kt = 0; kt < 4; ++kt) acc[T][kt] = mfma(afr_, bfr[kt], acc[T][kt]);     \
+    const s16x8 v_ = {xlo[TP][0], xlo[TP][1], xlo[TP][2], xlo[TP][3], xhi[TP][0], xhi[TP][1], xhi[TP][2], xhi[TP][3]}; \
+    const V8<T> afr_ = __builtin_bit_cast(V8<T>, v_);                                                \
+    _Pragma("unroll") for (int kt = 0; kt < 4; ++kt) acc[TP][kt] = mfma(afr_, bfr[kt], acc[TP][kt]);     \
   } while (0)
-#define SQR_TAP_NEXT(T)                                  \
+#define SQR_TAP_NEXT(TP)                                  \
   do {                                                   \
-    SQR_TAP(T);                                          \
-    SQR_X_READ(T + 2);                                   \
+    SQR_TAP(TP);                                          \
+    SQR_X_READ(TP + 2);                                   \
     asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");   \
     __builtin_amdgcn_sched_barrier(0);                   \
   } while (0)
@@ -1103,13 +1102,13 @@ bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) 
 }
 }  // namespace
 
-int conv3s2_dgrad_launch(const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho, int Wo,
-                         int K, int C, hipStream_t st) {
-  if (g_direct == 0) return 1;
+int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,
+                         int Wo, int K, int C, hipStream_t st) {
+  if (g_direct == 0) return kNotHandled;
   int TH, TW, BN, nch;
-  if (!s2_pick(Ho, Wo, K, C, &TH, &TW, &BN, &nch)) return 1;
+  if (!s2_pick(Ho, Wo, K, C, &TH, &TW, &BN, &nch)) return kNotHandled;
   const size_t dybytes = (size_t)N * Ho * Wo * K * 2, wbytes = (size_t)9 * C * K * 2;
-  if (dybytes >= (1u << 31) || (size_t)N * 4 * Ho * Wo * C * 2 >= (1u << 31)) return 1;
+  if (dybytes >= (1u << 31) || (size_t)N * 4 * Ho * Wo * C * 2 >= (1u << 31)) return kNotHandled;
   D3S2Args a;
   a.dy = dy;
   a.w = w_cls;
@@ -1131,25 +1130,27 @@ int conv3s2_dgrad_launch(const void* dy, const void* w_cls, const int* cls_off, 
   // slower
   const dim3 grid(N * a.tiles_per_img * a.ntn);
   probe_begin(st);
-  if (nch == 2)
-    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 32, 64, 4, 2, 2, 5>), grid, dim3(512), 0, st, a);
-  else if (nch == 8)
-    hipLaunchKernelGGL((conv3s2_dgrad_kernel<8, 8, 64, 2, 2, 8, 3>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv3s2_dgrad_kernel<4, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
+  SQR_DISPATCH16(dtype, T, {
+    if (nch == 2)
+      hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 32, 64, 4, 2, 2, 5>), grid, dim3(512), 0, st, a);
+    else if (nch == 8)
+      hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 8, 64, 2, 2, 8, 3>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 4, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
+  });
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3s2_dgrad_kernel");
   return 0;
 }
 
 
-// 1 = not applicable (caller falls back to the implicit-GEMM path), 0 = launched, else error
-int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
+// kNotHandled = not applicable (caller falls back to the implicit-GEMM path), 0 = launched, else error
+int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st) {
-  if (g_direct == 0) return 1;
-  if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return 1;
+  if (g_direct == 0) return kNotHandled;
+  if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return kNotHandled;
   const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
-  if (xbytes >= (1u << 31) || wbytes >= (1u << 31) || (size_t)N * H * W * Nout * 2 >= (1u << 31)) return 1;
+  if (xbytes >= (1u << 31) || wbytes >= (1u << 31) || (size_t)N * H * W * Nout * 2 >= (1u << 31)) return kNotHandled;
   if (Cin == 64 && Nout == 64 && W == 64 && H % 2 == 0 && g_persist) {
     static int ncu = 0;
     if (!ncu) {
@@ -1173,16 +1174,17 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
     p.flip = flip;
     p.xbytes = (uint32_t)xbytes;
     p.wbytes = (uint32_t)wbytes;
+    p.tp = probe_clock_take();
     const int grid = N * bpi;
     if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
     probe_begin(st);
-    hipLaunchKernelGGL(conv3p_kernel, dim3(grid), dim3(256), 0, st, p);
+    SQR_DISPATCH16(dtype, T, hipLaunchKernelGGL(conv3p_kernel<T>, dim3(grid), dim3(256), 0, st, p));
     probe_end(st);
     SQR_HIP_LAUNCH_CHECK("conv3p_kernel");
     return 0;
   }
   D3Cfg c;
-  if (!pick(N, H, W, Cin, Nout, &c)) return 1;
+  if (!pick(N, H, W, Cin, Nout, &c)) return kNotHandled;
   D3Args a;
   a.x = x;
   a.w = w;
@@ -1200,22 +1202,25 @@ int conv3_launch(const void* x, const void* w, void* out, int N, int H, int W, i
   a.flip = flip;
   a.xbytes = (uint32_t)xbytes;
   a.wbytes = (uint32_t)wbytes;
+  a.tp = probe_clock_take();
   if (stats_rows) *stats_rows = a.ntm;
   const dim3 grid(a.ntm * a.ntn), blk(c.threads);
   probe_begin(st);
-  switch (c.id) {
-    case 0: hipLaunchKernelGGL((conv3_kernel<256, 64, 4, 1, 64, 4, 1>), grid, blk, 0, st, a); break;
-    case 1: hipLaunchKernelGGL((conv3_kernel<256, 128, 4, 2, 32, 8, 2>), grid, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv3_kernel<128, 128, 4, 2, 16, 8, 2>), grid, blk, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((conv3_kernel<64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
-    case 4: hipLaunchKernelGGL((conv3_kernel<256, 64, 4, 1, 16, 16, 2>), grid, blk, 0, st, a); break;
-    case 5: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2>), grid, blk, 0, st, a); break;
-    case 6: hipLaunchKernelGGL((conv3_kernel<256, 32, 4, 1, 8, 8, 2, 4>), grid, blk, 0, st, a); break;
-    case 7: hipLaunchKernelGGL((conv3_kernel<256, 128, 4, 2, 32, 8, 2, 1, 3>), grid, blk, 0, st, a); break;
-    case 8: hipLaunchKernelGGL((conv3_kernel<128, 128, 4, 2, 16, 8, 2, 1, 5>), grid, blk, 0, st, a); break;
-    case 9: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2, 5>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3_kernel<128, 64, 2, 2, 8, 8, 2, 2, 8>), grid, blk, 0, st, a); break;
-  }
+  SQR_DISPATCH16(dtype, T, {
+    switch (c.id) {
+      case 0: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 64, 4, 1>), grid, blk, 0, st, a); break;
+      case 1: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2>), grid, blk, 0, st, a); break;
+      case 2: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2>), grid, blk, 0, st, a); break;
+      case 3: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
+      case 4: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 16, 16, 2>), grid, blk, 0, st, a); break;
+      case 5: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2>), grid, blk, 0, st, a); break;
+      case 6: hipLaunchKernelGGL((conv3_kernel<T, 256, 32, 4, 1, 8, 8, 2, 4>), grid, blk, 0, st, a); break;
+      case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 3>), grid, blk, 0, st, a); break;
+      case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5>), grid, blk, 0, st, a); break;
+      case 9: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 5>), grid, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8>), grid, blk, 0, st, a); break;
+    }
+  });
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_kernel");
   return 0;
@@ -1252,11 +1257,11 @@ size_t conv3w_slab_bytes(int N, int H, int W, int C, int K) {
   return (size_t)p.splits * K * 9 * C * sizeof(float);
 }
 
-int conv3w_launch(const void* x, const void* dy, float* slab, size_t slab_bytes, int N, int H, int W, int C, int K,
-                  int* splits, hipStream_t st) {
+int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t slab_bytes, int N, int H, int W, int C,
+                  int K, int* splits, hipStream_t st) {
   D3WPlan p;
-  if (!plan_w(N, H, W, C, K, &p)) return 1;
-  if ((size_t)p.splits * K * 9 * C * sizeof(float) > slab_bytes) return 1;
+  if (!plan_w(N, H, W, C, K, &p)) return kNotHandled;
+  if ((size_t)p.splits * K * 9 * C * sizeof(float) > slab_bytes) return kNotHandled;
   D3WArgs a;
   a.x = x;
   a.dy = dy;
@@ -1277,12 +1282,14 @@ int conv3w_launch(const void* x, const void* dy, float* slab, size_t slab_bytes,
   *splits = p.splits;
   const dim3 grid(p.splits * p.ntiles), blk(256);
   probe_begin(st);
-  switch (p.TW) {
-    case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<64, 2, 3>), grid, blk, 0, st, a); break;
-    case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<32, 4, 3>), grid, blk, 0, st, a); break;
-    case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<16, 8, 3>), grid, blk, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3_wgrad_kernel<8, 8, 4>), grid, blk, 0, st, a); break;
-  }
+  SQR_DISPATCH16(dtype, T, {
+    switch (p.TW) {
+      case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 64, 2, 3>), grid, blk, 0, st, a); break;
+      case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 32, 4, 3>), grid, blk, 0, st, a); break;
+      case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 16, 8, 3>), grid, blk, 0, st, a); break;
+      default: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 8, 8, 4>), grid, blk, 0, st, a); break;
+    }
+  });
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_wgrad_kernel");
   return 0;

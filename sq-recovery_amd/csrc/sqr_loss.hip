@@ -404,7 +404,8 @@ __global__ void __launch_bounds__(NT) explicit_loss_kernel(const float* __restri
 struct SQd {
   double a[3], e1, e2, ie1, ie2, r21, tr[3], M[9];
 };
-__device__ void sqd_load(const float* __restrict__ p, SQd& s) {
+template <typename P>
+__device__ void sqd_load(const P* __restrict__ p, SQd& s) {
   double raw[12];
   for (int i = 0; i < 12; ++i) raw[i] = (double)p[i];
   for (int i = 0; i < 3; ++i) s.a[i] = raw[i];
@@ -435,9 +436,10 @@ __device__ __forceinline__ bool sqd_inside(const SQd& s, double gx, double gy, d
   return pow(E + C, s.e1) <= 1.0;
 }
 
-template <int NT>
-__global__ void __launch_bounds__(NT) iou_kernel(const float* __restrict__ p_true,
-                                                 const float* __restrict__ p_pred, int R,
+// P = float (network outputs) or double (visu.py's float64 parameters, used without rounding)
+template <int NT, typename P>
+__global__ void __launch_bounds__(NT) iou_kernel(const P* __restrict__ p_true,
+                                                 const P* __restrict__ p_pred, int R,
                                                  unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long red[2 * (NT / 64)];
   const int b = blockIdx.y;
@@ -592,8 +594,8 @@ extern "C" int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pre
   return SQR_OK;
 }
 
-extern "C" int sqr_iou_counts(const float* p_true, const float* p_pred, int B, int R, long long* counts,
-                              void* stream) {
+template <typename P>
+static int iou_counts_impl(const P* p_true, const P* p_pred, int B, int R, long long* counts, void* stream) {
   SQR_CHECK_ARG(B >= 1 && B <= 65535 && R >= 1 && R <= 2048, "iou_counts: bad B=%d R=%d", B, R);
   SQR_CHECK_ARG(p_true && p_pred && counts, "iou_counts: null pointer");
   hipStream_t st = as_stream(stream);
@@ -603,8 +605,18 @@ extern "C" int sqr_iou_counts(const float* p_true, const float* p_pred, int B, i
     return (int)e;
   }
   const int nblk = (R * R + 255) / 256;
-  hipLaunchKernelGGL((iou_kernel<256>), dim3(nblk, B), dim3(256), 0, st, p_true, p_pred, R,
+  hipLaunchKernelGGL((iou_kernel<256, P>), dim3(nblk, B), dim3(256), 0, st, p_true, p_pred, R,
                      (unsigned long long*)counts);
   SQR_HIP_LAUNCH_CHECK("iou_kernel");
   return SQR_OK;
+}
+
+extern "C" int sqr_iou_counts(const float* p_true, const float* p_pred, int B, int R, long long* counts,
+                              void* stream) {
+  return iou_counts_impl<float>(p_true, p_pred, B, R, counts, stream);
+}
+
+extern "C" int sqr_iou_counts_f64(const double* p_true, const double* p_pred, int B, int R, long long* counts,
+                                  void* stream) {
+  return iou_counts_impl<double>(p_true, p_pred, B, R, counts, stream);
 }

@@ -1,4 +1,5 @@
-// Adam step fused with the bf16 weight packing of the conv kernels.
+// Adam step fused with the bf16 / fp16 weight packing of the conv kernels, and the dynamic
+// loss-scaling (torch.amp.GradScaler) pieces of the fp16 configuration.
 //
 // torch.optim.Adam (the optimizer of torch/train.py:50-54, lr 1e-4) updates every fp32 parameter;
 // the HIP convs then need each conv weight in two bf16 layouts (sqr_conv2d_pack_weight): [K][R][S][C]
@@ -20,6 +21,7 @@ namespace sqr {
 namespace optim {
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -30,9 +32,10 @@ struct Job {
   float *p, *m, *v;
   const float* g;
   const float* step;
-  bf16* krsc;       // conv weight: packed [K][R][S][C] (or [K][Kp] for C < 8), else null
+  void* krsc;       // conv weight: packed [K][R][S][C] (or [K][Kp] for C < 8), else null
   int n;            // elements
   int K, C, RS, Kp; // conv geometry (krsc != null)
+  int f16;          // krsc element type: 0 bf16, 1 fp16
 };
 struct Jobs {
   Job j[MAXJ];
@@ -42,6 +45,8 @@ struct Jobs {
   float fb2, eps;
   float omb1, omb2;    // 1 - b1, 1 - b2 (computed in double, as torch does)
   float gscale;        // gradients are used as g * gscale (1 = torch; 1/N averages summed data-parallel grads)
+  const float* loss_scale;  // nullable (device): gradients are also multiplied by 1 / *loss_scale
+  const int* found_inf;     // nullable (device): != 0 -> skip the whole step (GradScaler.step)
 };
 
 // torch's multi-tensor Adam, operation by operation (explicitly rounded: no fma contraction):
@@ -57,10 +62,13 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   extern __shared__ float lds[];
   const int b = blockIdx.x;
+  if (J.found_inf && *J.found_inf) return;  // non-finite scaled gradient somewhere: skip the step
   int ji = 0;
   while (ji + 1 < J.njobs && b >= J.start[ji + 1]) ++ji;
   const Job& jb = J.j[ji];
   const int local = b - J.start[ji];
+  // GradScaler's unscale: g * (1 / scale) with the reciprocal rounded to fp32 as torch does
+  const float gsc = J.loss_scale ? J.gscale * (float)(1.0 / (double)*J.loss_scale) : J.gscale;
   const double t = (double)(*jb.step) + 1.0;
   const double bc1 = 1.0 - pow(J.b1, t), bc2 = 1.0 - pow(J.b2, t);
   const float step_size = (float)(J.lr / bc1), bc2s = (float)sqrt(bc2);
@@ -69,7 +77,7 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
     const int i1 = min(i0 + CHUNK, jb.n);
     for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) {
       float p = jb.p[i], m = jb.m[i], v = jb.v[i];
-      adam_update(p, m, v, J.gscale == 1.f ? jb.g[i] : jb.g[i] * J.gscale, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+      adam_update(p, m, v, gsc == 1.f ? jb.g[i] : jb.g[i] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
       jb.p[i] = p;
       jb.m[i] = m;
       jb.v[i] = v;
@@ -81,7 +89,7 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   const size_t base = (size_t)k * CRS;
   for (int i = threadIdx.x; i < CRS; i += 256) {
     float p = jb.p[base + i], m = jb.m[base + i], v = jb.v[base + i];
-    adam_update(p, m, v, J.gscale == 1.f ? jb.g[base + i] : jb.g[base + i] * J.gscale, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+    adam_update(p, m, v, gsc == 1.f ? jb.g[base + i] : jb.g[base + i] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
     jb.p[base + i] = p;
     jb.m[base + i] = m;
     jb.v[base + i] = v;
@@ -89,20 +97,22 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   }
   __syncthreads();
   // krsc[k][tap][c] (row length Kp >= RS*C; the im2col padding is zero)
-  bf16* __restrict__ dst = jb.krsc + (size_t)k * jb.Kp;
   for (int i = threadIdx.x; i < jb.Kp; i += 256) {
     float val = 0.f;
     if (i < CRS) {
       const int tap = i / jb.C, c = i - tap * jb.C;
       val = lds[c * jb.RS + tap];
     }
-    dst[i] = (bf16)val;
+    if (jb.f16)
+      ((f16*)jb.krsc)[(size_t)k * jb.Kp + i] = (f16)val;
+    else
+      ((bf16*)jb.krsc)[(size_t)k * jb.Kp + i] = (bf16)val;
   }
 }
 
 struct CJob {
-  const bf16* krsc;  // [K][RS][C]
-  bf16* crsk;        // parity classes [C][Rc][Sc][K] back to back
+  const uint16_t* krsc;  // [K][RS][C] (bf16 or fp16 bits)
+  uint16_t* crsk;        // parity classes [C][Rc][Sc][K] back to back
   int K, C, R, S, st, pad;
   int cls_off[4];    // element offset of each stride-parity class
   int ntk, ntc;      // 64-wide tiles of K and C
@@ -113,13 +123,14 @@ struct CJobs {
   int njobs;
   float* steps[80];  // step counters to increment (block 0)
   int nsteps;
+  const int* found_inf;  // nullable: != 0 -> the step was skipped (counters stay)
 };
 
 // one workgroup per (job, tap, k tile, c tile): 64 x 64 bf16 transpose through LDS
 __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
   __shared__ uint16_t tile[64][66];
   const int b = blockIdx.x;
-  if (b == 0 && threadIdx.x < J.nsteps) *J.steps[threadIdx.x] += 1.f;
+  if (b == 0 && threadIdx.x < J.nsteps && !(J.found_inf && *J.found_inf)) *J.steps[threadIdx.x] += 1.f;
   if (J.njobs == 0) return;
   int ji = 0;
   while (ji + 1 < J.njobs && b >= J.start[ji + 1]) ++ji;
@@ -136,7 +147,7 @@ __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
   // load krsc[k0 + kk][tap][c0 .. c0 + 63]: thread = (kk = tid / 4, 16 channels)
   {
     const int kk = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
-    const uint16_t* src = (const uint16_t*)jb.krsc + ((size_t)(k0 + kk) * RS + tap) * jb.C + c0 + cc;
+    const uint16_t* src = jb.krsc + ((size_t)(k0 + kk) * RS + tap) * jb.C + c0 + cc;
 #pragma unroll
     for (int e = 0; e < 16; ++e) tile[kk][cc + e] = src[e];
   }
@@ -150,7 +161,7 @@ __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
   const int t = (r - r0) / st, u = (s - s0) / st;
   {
     const int cc = threadIdx.x >> 2, kk = (threadIdx.x & 3) * 16;
-    uint16_t* dst = (uint16_t*)jb.crsk + jb.cls_off[cl] + (((size_t)(c0 + cc) * Rc + t) * Sc + u) * jb.K + k0 + kk;
+    uint16_t* dst = jb.crsk + jb.cls_off[cl] + (((size_t)(c0 + cc) * Rc + t) * Sc + u) * jb.K + k0 + kk;
 #pragma unroll
     for (int e = 0; e < 16; ++e) dst[e] = tile[kk + e][cc];
   }
@@ -162,14 +173,16 @@ __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
 using namespace sqr;
 using namespace sqr::optim;
 
-extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2,
-                             double eps, double grad_scale, void* stream) {
+extern "C" int sqr_adam_step_amp(const sqr_adam_param* params, int nparams, double lr, double beta1,
+                                 double beta2, double eps, double grad_scale, const float* loss_scale,
+                                 const int* found_inf, void* stream) {
   SQR_CHECK_ARG(params && nparams >= 0 && nparams <= 80, "adam_step: 0 <= nparams <= 80");
   hipStream_t st = as_stream(stream);
   size_t maxlds = 16;
   CJobs cj;
   cj.njobs = 0;
   cj.nsteps = 0;
+  cj.found_inf = found_inf;
   int cblocks = 0;
   for (int i0 = 0; i0 < nparams; i0 += MAXJ) {
     Jobs J;
@@ -181,6 +194,8 @@ extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double l
     J.omb1 = (float)(1.0 - beta1);
     J.omb2 = (float)(1.0 - beta2);
     J.gscale = (float)grad_scale;
+    J.loss_scale = loss_scale;
+    J.found_inf = found_inf;
     J.njobs = 0;
     int blocks = 0;
     for (int i = i0; i < nparams && i < i0 + MAXJ; ++i) {
@@ -194,13 +209,15 @@ extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double l
       jb.v = q.exp_avg_sq;
       jb.step = q.step;
       jb.n = (int)q.n;
-      jb.krsc = (bf16*)q.w_krsc;
+      jb.krsc = q.w_krsc;
+      jb.f16 = q.desc.dtype == SQR_DTYPE_F16;
       jb.K = jb.C = jb.RS = jb.Kp = 0;
       int nb;
       if (q.w_krsc) {
         const sqr_conv_desc& d = q.desc;
-        SQR_CHECK_ARG(d.dtype == SQR_DTYPE_BF16 && (long long)d.K * d.C * d.R * d.S == q.n && d.stride <= 2,
-                      "adam_step: parameter %d: packing needs a bf16 descriptor matching the weight", i);
+        SQR_CHECK_ARG((d.dtype == SQR_DTYPE_BF16 || d.dtype == SQR_DTYPE_F16) &&
+                          (long long)d.K * d.C * d.R * d.S == q.n && d.stride <= 2,
+                      "adam_step: parameter %d: packing needs a bf16 / fp16 descriptor matching the weight", i);
         jb.K = d.K;
         jb.C = d.C;
         jb.RS = d.R * d.S;
@@ -217,8 +234,8 @@ extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double l
           SQR_CHECK_ARG(d.K % 64 == 0 && d.C % 64 == 0 && cj.njobs < 24,
                         "adam_step: parameter %d: dgrad packing needs K, C multiples of 64", i);
           CJob& c = cj.j[cj.njobs];
-          c.krsc = (const bf16*)q.w_krsc;
-          c.crsk = (bf16*)q.w_crsk;
+          c.krsc = (const uint16_t*)q.w_krsc;
+          c.crsk = (uint16_t*)q.w_crsk;
           c.K = d.K;
           c.C = d.C;
           c.R = d.R;
@@ -256,5 +273,108 @@ extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double l
   const int cb = cblocks > 1 ? cblocks : 1;
   hipLaunchKernelGGL(crsk_kernel, dim3(cb), dim3(256), 0, st, cj);
   SQR_HIP_LAUNCH_CHECK("crsk_kernel");
+  return 0;
+}
+
+extern "C" int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2,
+                             double eps, double grad_scale, void* stream) {
+  return sqr_adam_step_amp(params, nparams, lr, beta1, beta2, eps, grad_scale, nullptr, nullptr, stream);
+}
+
+// ---------------------------------------------------------------- dynamic loss scaling
+
+namespace sqr {
+namespace optim {
+
+constexpr int MAXF = 80;
+struct FJobs {
+  const float* g[MAXF];
+  long long n[MAXF];
+  int start[MAXF + 1];  // first workgroup of each tensor
+  int nj;
+  int* found_inf;
+};
+constexpr int FCHUNK = 16384;  // elements per workgroup
+
+// found_inf |= any(!isfinite(g)) over every tensor (GradScaler's unscale_ check; the unscale
+// multiply itself is folded into the Adam kernel)
+__global__ void __launch_bounds__(256) amp_check_kernel(FJobs J) {
+  const int b = blockIdx.x;
+  int ji = 0;
+  while (ji + 1 < J.nj && b >= J.start[ji + 1]) ++ji;
+  const long long i0 = (long long)(b - J.start[ji]) * FCHUNK;
+  const long long i1 = i0 + FCHUNK < J.n[ji] ? i0 + FCHUNK : J.n[ji];
+  const float* g = J.g[ji];
+  bool bad = false;
+  if (((uintptr_t)g & 15) == 0) {
+    const long long v1 = i0 + ((i1 - i0) & ~3ll);
+    for (long long i = i0 + 4 * threadIdx.x; i < v1; i += 4 * 256) {
+      const f32x4 v = *(const f32x4*)(g + i);
+      // x - x is NaN for inf and NaN inputs, 0 otherwise (no isfinite on the vector path)
+      bad |= !((v[0] - v[0]) == 0.f) | !((v[1] - v[1]) == 0.f) | !((v[2] - v[2]) == 0.f) | !((v[3] - v[3]) == 0.f);
+    }
+    for (long long i = v1 + threadIdx.x; i < i1; i += 256) bad |= !((g[i] - g[i]) == 0.f);
+  } else {
+    for (long long i = i0 + threadIdx.x; i < i1; i += 256) bad |= !((g[i] - g[i]) == 0.f);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(J.found_inf, 1);
+}
+
+// GradScaler.update(): backoff on overflow, grow after `interval` clean steps; then clear found_inf
+// for the next step
+__global__ void amp_update_kernel(float* scale, int* tracker, int* found_inf, float growth, float backoff,
+                                  int interval) {
+  if (threadIdx.x != 0) return;
+  if (*found_inf) {
+    *scale = *scale * backoff;
+    *tracker = 0;
+  } else {
+    const int t = *tracker + 1;
+    if (t == interval) {
+      const float s = *scale * growth;
+      // torch keeps the old scale when growing would overflow fp32
+      if (s - s == 0.f) *scale = s;
+      *tracker = 0;
+    } else {
+      *tracker = t;
+    }
+  }
+  *found_inf = 0;
+}
+
+}  // namespace optim
+}  // namespace sqr
+
+extern "C" int sqr_amp_check_finite(const float* const* grads, const long long* sizes, int n, int* found_inf,
+                                    void* stream) {
+  SQR_CHECK_ARG(grads && sizes && found_inf && n >= 0, "amp_check_finite: null argument");
+  hipStream_t st = as_stream(stream);
+  for (int i0 = 0; i0 < n; i0 += MAXF) {
+    FJobs J;
+    J.nj = 0;
+    J.found_inf = found_inf;
+    int blocks = 0;
+    for (int i = i0; i < n && i < i0 + MAXF; ++i) {
+      SQR_CHECK_ARG(grads[i] && sizes[i] > 0, "amp_check_finite: tensor %d: null pointer or empty", i);
+      J.g[J.nj] = grads[i];
+      J.n[J.nj] = sizes[i];
+      J.start[J.nj] = blocks;
+      blocks += (int)((sizes[i] + FCHUNK - 1) / FCHUNK);
+      ++J.nj;
+    }
+    J.start[J.nj] = blocks;
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(amp_check_kernel, dim3(blocks), dim3(256), 0, st, J);
+    SQR_HIP_LAUNCH_CHECK("amp_check_kernel");
+  }
+  return 0;
+}
+
+extern "C" int sqr_amp_update_scale(float* scale, int* growth_tracker, int* found_inf, float growth_factor,
+                                    float backoff_factor, int growth_interval, void* stream) {
+  SQR_CHECK_ARG(scale && growth_tracker && found_inf && growth_interval > 0, "amp_update_scale: bad argument");
+  hipLaunchKernelGGL(amp_update_kernel, dim3(1), dim3(64), 0, as_stream(stream), scale, growth_tracker, found_inf,
+                     growth_factor, backoff_factor, growth_interval);
+  SQR_HIP_LAUNCH_CHECK("amp_update_kernel");
   return 0;
 }

@@ -24,6 +24,7 @@ namespace sqr {
 namespace tail {
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int MAXF = 1024;  // max features of any tail layer (C0, F1, F2)
@@ -59,6 +60,21 @@ template <> struct IO<bf16> {
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
     *(bf16x8*)p = o;
+  }
+};
+template <> struct IO<f16> {
+  static __device__ __forceinline__ void load8(const f16* p, float* v) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    const f16x8 u = *(const f16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)u[i];
+  }
+  static __device__ __forceinline__ void store8(f16* p, const float* v) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    f16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (f16)v[i];
+    *(f16x8*)p = o;
   }
 };
 template <> struct IO<float> {
@@ -348,7 +364,8 @@ int check_tail(const sqr_tail_desc* t) {
                 t->C0, MAXF);
   SQR_CHECK_ARG(t->F1 >= 4 && t->F1 <= MAXF && t->F1 % 4 == 0 && t->F2 >= 4 && t->F2 <= MAXF && t->F2 % 4 == 0,
                 "tail: F1=%d F2=%d must be multiples of 4 in [4, %d]", t->F1, t->F2, MAXF);
-  SQR_CHECK_ARG(t->dtype == SQR_DTYPE_F32 || t->dtype == SQR_DTYPE_BF16, "tail: bad dtype");
+  SQR_CHECK_ARG(t->dtype == SQR_DTYPE_F32 || t->dtype == SQR_DTYPE_BF16 || t->dtype == SQR_DTYPE_F16,
+                "tail: bad dtype");
   SQR_CHECK_ARG(t->w0 && t->b0 && t->w1 && t->b1, "tail: null fc parameter");
   for (int h = 0; h < 4; ++h) SQR_CHECK_ARG(t->wh[h] && t->bh[h], "tail: null head %d parameter", h);
   SQR_CHECK_ARG((size_t)t->B * t->P * t->C0 < (1ull << 31), "tail: activation too large");
@@ -395,6 +412,8 @@ extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a,
   hipStream_t st = as_stream(stream);
   if (t->dtype == SQR_DTYPE_BF16)
     hipLaunchKernelGGL(tail_fwd_kernel<bf16>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
+  else if (t->dtype == SQR_DTYPE_F16)
+    hipLaunchKernelGGL(tail_fwd_kernel<f16>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
   else
     hipLaunchKernelGGL(tail_fwd_kernel<float>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
   SQR_HIP_LAUNCH_CHECK("tail_fwd_kernel");
@@ -432,6 +451,8 @@ extern "C" int sqr_tail_bwd(const sqr_tail_desc* t, const float* save, const sqr
   hipStream_t st = as_stream(stream);
   if (t->dtype == SQR_DTYPE_BF16)
     hipLaunchKernelGGL(tail_bwd_kernel<bf16>, dim3(t->B), dim3(256), 0, st, d, save, up, (bf16*)g->dx, dsave);
+  else if (t->dtype == SQR_DTYPE_F16)
+    hipLaunchKernelGGL(tail_bwd_kernel<f16>, dim3(t->B), dim3(256), 0, st, d, save, up, (f16*)g->dx, dsave);
   else
     hipLaunchKernelGGL(tail_bwd_kernel<float>, dim3(t->B), dim3(256), 0, st, d, save, up, (float*)g->dx, dsave);
   SQR_HIP_LAUNCH_CHECK("tail_bwd_kernel");

@@ -1,14 +1,15 @@
-"""Drop-in for torch/helpers.py (timoblak/sq-recovery): checkpoints, label parsing, scanner
-command lines and plotting utilities.
+"""Drop-in for torch/helpers.py (timoblak/sq-recovery): checkpoints, label parsing and scanner
+command lines — the parts train.py / test.py use.  The reference's plotting and autograd-debug
+utilities (plot_render, plot_points, gray_to_jet, plot_grad_flow, getBack, slerp, randquat;
+helpers.py:108-320) are out of scope and not restated.
 
 Checkpoint format is the reference's (helpers.py:42-68):
     {'epoch', 'model_state_dict', 'optimizer_state_dict', 'loss'}
 with un-prefixed state-dict keys; a DistributedDataParallel model is unwrapped before saving, so
-single-GPU and 8-GPU runs write interchangeable files.  Plotting helpers import matplotlib and
-the scanner helpers cv2 lazily (neither is needed on the training path).
+single-GPU and 8-GPU runs write interchangeable files.  The scanner helpers import cv2 lazily (it
+is not needed on the training path).
 """
 import os
-from time import sleep
 
 import numpy as np
 import torch
@@ -129,32 +130,6 @@ def change_lr(opt, lr):
         g["lr"] = lr
 
 
-def plot_render(meshgrid, np_array, mode="all", figure=1, lims=(0, 1), eps=0.1):
-    """helpers.py:108-173 (3-D scatter of an occupancy/inside-outside volume)."""
-    from matplotlib import pyplot as plt
-    from mpl_toolkits.mplot3d import Axes3D  # noqa: F401
-    masks = {"all": np_array >= 0, "in": np_array <= 1, "in_inv": np_array > 0.9, "bit": np_array == 1,
-             "shell": (np_array < 1 + eps) & (np_array > 1 - eps)}
-    disp = masks[mode].ravel()
-    v = np_array.ravel()
-    vn = -1 + (v - v.min()) / (v.max() - v.min()) * 2
-    clr = np.array([gray_to_jet(x) for x in vn])
-    clr[:, 3] = np.where(disp, 1.0, 0.2 if mode in ("in", "in_inv") else 0.0)
-    ax = plt.figure(figure).add_subplot(1, 1, 1, projection="3d")
-    ax.scatter(meshgrid[0], meshgrid[1], meshgrid[2], color=clr, marker="o")
-    ax.set(xlim=lims, ylim=lims, zlim=lims)
-
-
-def plot_points(xs, ys, zs, figure=2, lims=(-1, 1), subplot=111):
-    from matplotlib import pyplot as plt
-    ax = plt.figure(figure).add_subplot(subplot, projection="3d")
-    ax.scatter(xs, ys, zs, marker="o")
-    ax.set(xlim=lims, ylim=lims, zlim=lims)
-    ax.set_xlabel("X Axis")
-    ax.set_ylabel("Y Axis")
-    ax.set_zlabel("Z Axis")
-
-
 def parse_csv(csvfile):
     """helpers.py:188-218: rows 'fn,a1,a2,a3,e1,e2,t1,t2,t3,m11..m33,q1..q4' ->
     float32 [a/255 (3), e (2), t/255 (3), q (4)] per image."""
@@ -172,76 +147,3 @@ def parse_csv(csvfile):
     print("Size of data: " + str(len(labels)))
     print("----------------------------------------------------------------")
     return labels
-
-
-def gray_to_jet(gray):
-    """helpers.py:221-239: value in [-1,1] -> (r, g, b, a) of the jet colormap."""
-    def base(val):
-        if val <= -0.75:
-            return 0.0
-        if val <= -0.25:
-            return (val + 0.75) / 0.5
-        if val <= 0.25:
-            return 1.0
-        if val <= 0.75:
-            return 1.0 - (val - 0.25) / 0.5
-        return 0.0
-    return base(gray - 0.5), base(gray), base(gray + 0.5), 1
-
-
-def plot_grad_flow(named_parameters):
-    """helpers.py:242-268: bar plot of mean/max |grad| per weight tensor."""
-    from matplotlib import pyplot as plt
-    layers, ave, mx = [], [], []
-    for n, p in named_parameters:
-        if p.requires_grad and "bias" not in n and p.grad is not None:
-            layers.append(n)
-            ave.append(p.grad.abs().mean().item())
-            mx.append(p.grad.abs().max().item())
-    plt.bar(np.arange(len(mx)), mx, alpha=0.1, lw=1, color="c")
-    plt.bar(np.arange(len(mx)), ave, alpha=0.1, lw=1, color="b")
-    plt.xticks(range(len(ave)), layers, rotation="vertical")
-    plt.title("Gradient flow")
-
-
-def getBack(var_grad_fn):
-    """helpers.py:271-283: walk an autograd graph printing leaf gradients."""
-    print(var_grad_fn)
-    for n in var_grad_fn.next_functions:
-        if n[0]:
-            try:
-                sleep(1)
-                tensor = getattr(n[0], "variable")
-                print(n[0])
-                print("Tensor with grad found:", tensor)
-                print(" - gradient:", tensor.grad)
-                print()
-            except AttributeError:
-                getBack(n[0])
-
-
-def randquat():
-    """helpers.py:286-292."""
-    u = np.random.uniform(0, 1, (3,))
-    a, b = np.sqrt(1 - u[0]), np.sqrt(u[0])
-    return np.array([a * np.sin(2 * np.pi * u[1]), a * np.cos(2 * np.pi * u[1]),
-                     b * np.sin(2 * np.pi * u[2]), b * np.cos(2 * np.pi * u[2])])
-
-
-def slerp(v0, v1, t_array):
-    """helpers.py:295-320: spherical linear interpolation."""
-    t_array = np.array(t_array)
-    v0 = np.array(v0)
-    v1 = np.array(v1)
-    dot = np.sum(v0 * v1)
-    if dot < 0.0:
-        v1 = -v1
-        dot = -dot
-    if dot > 0.9995:
-        result = v0[np.newaxis, :] + t_array[:, np.newaxis] * (v1 - v0)[np.newaxis, :]
-        return (result.T / np.linalg.norm(result, axis=1)).T
-    theta_0 = np.arccos(dot)
-    theta = theta_0 * t_array
-    s0 = np.cos(theta) - dot * np.sin(theta) / np.sin(theta_0)
-    s1 = np.sin(theta) / np.sin(theta_0)
-    return (s0[:, np.newaxis] * v0[np.newaxis, :]) + (s1[:, np.newaxis] * v1[np.newaxis, :]), v1

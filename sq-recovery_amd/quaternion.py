@@ -27,12 +27,14 @@ def conjugate_np(quaternion):
 
 
 def _hamilton(q1, q2, stack):
+    # terms summed left to right in the reference's order (quaternion.py:30-33), so the float64
+    # results are bitwise the reference's
     x1, y1, z1, w1 = q1
     x2, y2, z2, w2 = q2
-    return stack([w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
-                  w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
-                  w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2,
-                  w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2])
+    return stack([x1 * w2 + y1 * z2 - z1 * y2 + w1 * x2,
+                  -x1 * z2 + y1 * w2 + z1 * x2 + w1 * y2,
+                  x1 * y2 - y1 * x2 + z1 * w2 + w1 * z2,
+                  -x1 * x2 - y1 * y2 - z1 * z2 + w1 * w2])
 
 
 def multiply(quaternion1, quaternion2):

@@ -51,6 +51,8 @@ SIGNATURES = {
     "sqr_version": (c_int, []),
     "sqr_last_error_string": (ctypes.c_char_p, []),
     "sqr_probe_arm": (c_int, [c_void_p, c_void_p]),
+    "sqr_probe_arm_clock": (c_int, [c_void_p]),
+    "sqr_wall_clock_khz": (c_int, [ctypes.POINTER(c_int)]),
     "sqr_implicit_loss_workspace_bytes": (c_size_t, [c_int, c_int]),
     "sqr_implicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float,
                                           c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -59,6 +61,7 @@ SIGNATURES = {
     "sqr_explicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                           c_void_p, c_size_t, c_void_p]),
     "sqr_iou_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "sqr_iou_counts_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sqr_conv2d_out_hw": (c_int, [ctypes.POINTER(SqrConvDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "sqr_conv2d_workspace_bytes": (c_size_t, [ctypes.POINTER(SqrConvDesc), c_int]),
     "sqr_conv2d_pack_weight": (c_int, [c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_void_p, c_void_p]),
@@ -103,6 +106,11 @@ SIGNATURES = {
                                    c_void_p]),
     "sqr_adam_step": (c_int, [ctypes.POINTER(SqrAdamParam), c_int, c_double, c_double, c_double, c_double,
                               c_double, c_void_p]),
+    "sqr_adam_step_amp": (c_int, [ctypes.POINTER(SqrAdamParam), c_int, c_double, c_double, c_double, c_double,
+                                  c_double, c_void_p, c_void_p, c_void_p]),
+    "sqr_amp_check_finite": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong), c_int, c_void_p,
+                                     c_void_p]),
+    "sqr_amp_update_scale": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p]),
     "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p]),

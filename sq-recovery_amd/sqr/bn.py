@@ -17,11 +17,10 @@ _CL = torch.channels_last
 
 
 def _dt(t):
-    if t.dtype == torch.bfloat16:
-        return 1
-    if t.dtype == torch.float32:
-        return 0
-    raise TypeError("sqr bn: unsupported dtype %s" % t.dtype)
+    dt = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(t.dtype)
+    if dt is None:
+        raise TypeError("sqr bn: unsupported dtype %s" % t.dtype)
+    return dt
 
 
 def _momentum(bn):
@@ -254,7 +253,7 @@ class FusedStemFn(torch.autograd.Function):
 
 
 def fused_stem_ok(x, conv, bn):
-    """The fused stem applies: bf16 compute, 1-channel input that needs no gradient, the resnet18
+    """The fused stem applies: bf16 compute (fp16 takes the unfused conv1 + stem path), 1-channel input that needs no gradient, the resnet18
     conv1 geometry (64 x 1 x 7 x 7, stride 2, pad 3, no bias) and a tileable input size."""
     if not x.is_cuda or x.requires_grad or x.dim() != 4 or x.shape[1] != 1:
         return False

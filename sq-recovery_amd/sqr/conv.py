@@ -5,8 +5,8 @@ Activations are NHWC in memory (torch channels_last); the fp32 master weight sta
 torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
 ([K,R,S,C] for fwd, [C,R,S,K] for backward-data) in the compute dtype.
 
-Compute dtype: bfloat16 when the input is bf16 or CUDA autocast is on with bf16, else float32
-(exact-f32 MFMA: the parity mode).
+Compute dtype: bfloat16 / float16 when the input has that dtype or CUDA autocast is on with it,
+else float32 (exact-f32 MFMA: the parity mode).
 """
 import torch
 import torch.nn as nn
@@ -14,44 +14,71 @@ import torch.nn as nn
 from . import gradbuf
 from ._lib import SqrConvDesc, SqrPackJob, check, lib, ptr, stream_ptr
 
-DT_F32, DT_BF16 = 0, 1
+DT_F32, DT_BF16, DT_F16 = 0, 1, 2
+_DT = {torch.float32: DT_F32, torch.bfloat16: DT_BF16, torch.float16: DT_F16}
+_TORCH_DT = {v: k for k, v in _DT.items()}
 _CL = torch.channels_last
 
-# Optional kernel probe (bench.py): HIP events recorded by libsqr on the launch stream around the
-# main kernel of every call of one (phase, conv shape) — sqr_probe_arm — to time that kernel live
-# inside a training step (the split-K reduction / im2col launches of the call are outside).
-_probe = {"key": None, "events": []}
+# Optional kernel probe (bench.py) of the main kernel of every call of one (phase, conv shape), to
+# time that kernel live inside a training step (the split-K reduction / im2col launches of the call
+# are outside):
+#   events: HIP events recorded by libsqr on the launch stream around the kernel (sqr_probe_arm;
+#           eager steps only — inside a captured graph they cannot bracket one kernel node);
+#   clock:  rows of an int64 device tensor [n, 2] receiving the kernel's own wall-clock span
+#           (sqr_probe_arm_clock; works inside replayed graphs: the slot pointer is a kernel argument).
+_probe = {"key": None, "events": [], "clock": None, "nclock": 0}
 
 
-def set_probe(phase, N, C, H, K, R, stride):
-    """phase in {'fwd','dgrad','wgrad'}; shape as the conv's (N, C, H, K, R, stride)."""
+def set_probe(phase, N, C, H, K, R, stride, clock=None):
+    """phase in {'fwd','dgrad','wgrad'}; shape as the conv's (N, C, H, K, R, stride).  clock: an
+    int64 [n, 2] device tensor; matched calls then arm its rows in order (instead of events)."""
     _probe["key"] = (phase, N, C, H, K, R, stride)
     _probe["events"] = []
+    _probe["clock"] = clock
+    _probe["nclock"] = 0
 
 
 def probe_events():
     return _probe["events"]
 
 
+def probe_clock_rows():
+    """Number of clock rows armed since set_probe."""
+    return _probe["nclock"]
+
+
 class _Probe:
     def __init__(self, phase, d):
         self.on = _probe["key"] == (phase, d.N, d.C, d.H, d.K, d.R, d.stride)
+        clk = _probe["clock"]
+        if self.on and clk is not None and _probe["nclock"] >= clk.shape[0]:
+            self.on = False  # every clock row in use
 
     def __enter__(self):
-        if self.on:
-            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for e in self.ev:  # materialise the hipEvent_t (torch creates it lazily on first record)
-                e.record()
-            check(lib().sqr_probe_arm(self.ev[0].cuda_event, self.ev[1].cuda_event), "sqr_probe_arm")
+        if not self.on:
+            return
+        clk = _probe["clock"]
+        if clk is not None:
+            check(lib().sqr_probe_arm_clock(clk[_probe["nclock"]].data_ptr()), "sqr_probe_arm_clock")
+            _probe["nclock"] += 1
+            return
+        self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        for e in self.ev:  # materialise the hipEvent_t (torch creates it lazily on first record)
+            e.record()
+        check(lib().sqr_probe_arm(self.ev[0].cuda_event, self.ev[1].cuda_event), "sqr_probe_arm")
 
     def __exit__(self, *exc):
-        if self.on:
-            lib().sqr_probe_arm(None, None)
-            _probe["events"].append(self.ev)
+        if not self.on:
+            return
+        if _probe["clock"] is not None:
+            lib().sqr_probe_arm_clock(None)  # a call routed to a kernel without the probe leaves it armed
+            return
+        lib().sqr_probe_arm(None, None)
+        _probe["events"].append(self.ev)
 
 
 def _desc(N, C, H, W, K, R, S, stride, pad, dtype):
-    return SqrConvDesc(N, C, H, W, K, R, S, stride, pad, DT_BF16 if dtype == torch.bfloat16 else DT_F32)
+    return SqrConvDesc(N, C, H, W, K, R, S, stride, pad, _DT[dtype])
 
 
 def _out_hw(d):
@@ -70,7 +97,7 @@ def _ws(d, which, device):
 def pack_weight(weight, d, need_crsk):
     import ctypes
     K, C, R, S = weight.shape
-    dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+    dt = _TORCH_DT[d.dtype]
     w = weight.detach().to(torch.float32).contiguous()
     if C < 8:
         kp = 64
@@ -147,17 +174,13 @@ def pack_all(convs, dtype):
         mark_packed(m, dtype)
 
 
-def clear_packed(convs):
-    """(kept for API compatibility: packed weights are persistent per module and dtype)"""
-
-
 def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
     """y = conv(x); with return_ws the workspace (holding the im2col matrix for C<8) is returned
     too; with stats the BatchNorm partials [rows, 2, K] (f32 per-tile sum / sum of squares of y,
     see sqr_conv2d_fwd_stats) are returned after y."""
     import ctypes
     ho, wo = _out_hw(d)
-    dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+    dt = _TORCH_DT[d.dtype]
     y = torch.empty((d.N, d.K, ho, wo), dtype=dt, device=x.device, memory_format=_CL)
     ws, n = _ws(d, 0, x.device)
     st = None
@@ -181,7 +204,7 @@ def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
 
 def conv2d_bwd_data(gy, w_crsk, d):
     import ctypes
-    dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+    dt = _TORCH_DT[d.dtype]
     dx = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=gy.device, memory_format=_CL)
     ws, n = _ws(d, 1, gy.device)
     with _Probe("dgrad", d):
@@ -213,10 +236,12 @@ def conv2d_bwd_weight(x, gy, d, col=None, wid=None):
 
 
 def compute_dtype(x):
-    if x.dtype == torch.bfloat16:
-        return torch.bfloat16
-    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
-        return torch.bfloat16
+    if x.dtype in (torch.bfloat16, torch.float16):
+        return x.dtype
+    if torch.is_autocast_enabled("cuda"):
+        adt = torch.get_autocast_dtype("cuda")
+        if adt in (torch.bfloat16, torch.float16):
+            return adt
     return torch.float32
 
 
@@ -261,7 +286,7 @@ class Conv2dFn(torch.autograd.Function):
             return None, None, None, None, None, None, None, None
         xin, crsk, col = ctx.saved_tensors
         d = ctx.d
-        dt = torch.bfloat16 if d.dtype == DT_BF16 else torch.float32
+        dt = _TORCH_DT[d.dtype]
         g = gy.to(dt).contiguous(memory_format=_CL)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:

@@ -111,11 +111,14 @@ def implicit_render(params, R, tau=1.0, sharpness=100.0):
 
 
 def iou_counts(p_true, p_pred, R):
-    """[B,2] int64 (intersection, union) voxel counts of IoUAccuracy (classes.py:394-447)."""
+    """[B,2] int64 (intersection, union) voxel counts of IoUAccuracy (classes.py:394-447).  The
+    kernel works in float64 like the reference; float64 parameters (visu.py) are used as given."""
     _require_cuda(p_true, p_pred)
-    pt = p_true.detach().to(torch.float32).contiguous()
-    pp = p_pred.detach().to(torch.float32).contiguous()
+    f64 = p_true.dtype == torch.float64 or p_pred.dtype == torch.float64
+    dt = torch.float64 if f64 else torch.float32
+    pt = p_true.detach().to(dt).contiguous()
+    pp = p_pred.detach().to(dt).contiguous()
     out = torch.empty(pt.shape[0], 2, dtype=torch.int64, device=pt.device)
-    check(lib().sqr_iou_counts(ptr(pt), ptr(pp), pt.shape[0], int(R), ptr(out), stream_ptr(pt.device)),
-          "sqr_iou_counts")
+    fn = lib().sqr_iou_counts_f64 if f64 else lib().sqr_iou_counts
+    check(fn(ptr(pt), ptr(pp), pt.shape[0], int(R), ptr(out), stream_ptr(pt.device)), "sqr_iou_counts")
     return out

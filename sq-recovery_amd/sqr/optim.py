@@ -15,8 +15,8 @@ implementation (capturable mode, device step counters).
 """
 import torch
 
-from ._lib import SqrAdamParam, check, lib, stream_ptr
-from .conv import DT_BF16, Conv2d, _desc, mark_packed, packed_buffers
+from ._lib import SqrAdamParam, check, lib, ptr, stream_ptr
+from .conv import DT_BF16, DT_F16, Conv2d, _desc, mark_packed, packed_buffers
 
 
 class Adam(torch.optim.Adam):
@@ -31,9 +31,12 @@ class Adam(torch.optim.Adam):
         # gradients are read as g * grad_scale (sqr.dist.GraphDataParallel sets 1/world after a SUM
         # all-reduce; the fallback path requires 1)
         self.sqr_grad_scale = 1.0
+        # (loss scale or None, found_inf) device tensors while sqr.amp.GradScaler.step runs
+        self.sqr_amp = None
 
     def attach(self, model, dtype=torch.bfloat16):
-        """Pack the conv weights of `model` (sqr Conv2d modules) for `dtype` inside every step."""
+        """Pack the conv weights of `model` (sqr Conv2d modules) for `dtype` (bf16 / fp16) inside
+        every step."""
         for m in model.modules():
             if isinstance(m, Conv2d):
                 self._convs[id(m.weight)] = (m, dtype)
@@ -67,6 +70,9 @@ class Adam(torch.optim.Adam):
                 p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and not p.grad.is_sparse
                 and p.grad.dtype == torch.float32 and p.grad.is_contiguous() for p in ps)
             if not ok:
+                if self.sqr_amp is not None:
+                    raise RuntimeError("sqr Adam: loss scaling needs the fused path (fp32 CUDA params, "
+                                       "weight_decay 0, no amsgrad/maximize)")
                 if self.sqr_grad_scale != 1.0:
                     raise RuntimeError("sqr Adam: grad_scale != 1 needs the fused path (fp32 CUDA params, "
                                        "weight_decay 0, no amsgrad/maximize)")
@@ -94,12 +100,22 @@ class Adam(torch.optim.Adam):
                         krsc, crsk = packed_buffers(m, dt)
                         K, C, R, S = p.shape
                         a.desc = _desc(1, C, R, R, K, R, S, m.stride[0], m.padding[0], dt)
-                        if a.desc.dtype == DT_BF16 and (C < 8 or (K % 64 == 0 and C % 64 == 0)):
+                        if a.desc.dtype in (DT_BF16, DT_F16) and (C < 8 or (K % 64 == 0 and C % 64 == 0)):
                             a.w_krsc = krsc.data_ptr()
                             a.w_crsk = crsk.data_ptr() if crsk is not None else None
                             packed.append((m, dt))
-                check(L.sqr_adam_step(arr, len(chunk), lr, float(b1), float(b2), float(group["eps"]),
-                                      float(self.sqr_grad_scale), stream_ptr(chunk[0].device)), "sqr_adam_step")
+                if self.sqr_amp is not None:
+                    scale, found_inf = self.sqr_amp
+                    check(L.sqr_adam_step_amp(arr, len(chunk), lr, float(b1), float(b2), float(group["eps"]),
+                                              float(self.sqr_grad_scale), ptr(scale), ptr(found_inf),
+                                              stream_ptr(chunk[0].device)), "sqr_adam_step_amp")
+                else:
+                    check(L.sqr_adam_step(arr, len(chunk), lr, float(b1), float(b2), float(group["eps"]),
+                                          float(self.sqr_grad_scale), stream_ptr(chunk[0].device)), "sqr_adam_step")
+                # the kernel wrote the parameters through raw pointers: bump their version counters
+                # so every cache keyed on them (sqr.conv's packed weights of convs this step did not
+                # pack itself) sees the update
+                torch.autograd.graph.increment_version(chunk)
                 for m, dt in packed:
                     mark_packed(m, dt)
         return loss

@@ -21,7 +21,7 @@ def _desc(x, w0, b0, w1, b1, heads):
     B, C0, H, W = x.shape
     d = SqrTailDesc()
     d.B, d.P, d.C0, d.F1, d.F2 = B, H * W, C0, w0.shape[0], w1.shape[0]
-    d.dtype = 1 if x.dtype == torch.bfloat16 else 0
+    d.dtype = {torch.bfloat16: 1, torch.float16: 2}.get(x.dtype, 0)
     d.w0, d.b0, d.w1, d.b1 = w0.data_ptr(), b0.data_ptr(), w1.data_ptr(), b1.data_ptr()
     for i in range(4):
         d.wh[i] = heads[2 * i].data_ptr()

@@ -27,7 +27,7 @@ def _bn(C, seed):
     return bn
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
 @pytest.mark.parametrize("cfg", [(4, 64, 16, True, False), (2, 128, 9, True, True), (3, 512, 4, False, False),
                                  (2, 256, 8, False, True), (1, 8, 5, True, True)],
                          ids=lambda c: "N%dC%dH%d_relu%d_res%d" % c)
@@ -39,9 +39,9 @@ def test_bn_act(cfg, dtype, training):
     x = (torch.randn(N, C, H, H, generator=g) * 2 + 0.5)
     r = torch.randn(N, C, H, H, generator=g) if res else None
     gy = torch.randn(N, C, H, H, generator=g)
-    if dtype == torch.bfloat16:
-        x, gy = x.bfloat16().float(), gy.bfloat16().float()
-        r = r.bfloat16().float() if r is not None else None
+    if dtype != torch.float32:
+        x, gy = x.to(dtype).float(), gy.to(dtype).float()
+        r = r.to(dtype).float() if r is not None else None
     bn_ref = _bn(C, 1).double().train(training)
     bn_gpu = copy.deepcopy(_bn(C, 1)).to(DEV).train(training)
     xr = x.double().requires_grad_(True)
@@ -70,19 +70,19 @@ def test_bn_act(cfg, dtype, training):
     assert int(bn_gpu.num_batches_tracked) == int(bn_ref.num_batches_tracked)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
 @pytest.mark.parametrize("shape", [(2, 64, 32), (3, 64, 17), (1, 8, 6)], ids=lambda s: "N%dC%dH%d" % s)
 def test_stem_bn_relu_maxpool(shape, dtype):
     from sqr.bn import stem
     N, C, H = shape
     g = torch.Generator().manual_seed(H)
     x = torch.randn(N, C, H, H, generator=g)
-    if dtype == torch.bfloat16:
-        x = x.bfloat16().float()
+    if dtype != torch.float32:
+        x = x.to(dtype).float()
     Ho = (H - 1) // 2 + 1
     gy = torch.randn(N, C, Ho, Ho, generator=g)
-    if dtype == torch.bfloat16:
-        gy = gy.bfloat16().float()
+    if dtype != torch.float32:
+        gy = gy.to(dtype).float()
     bn_ref = _bn(C, 2).double().train()
     bn_gpu = _bn(C, 2).to(DEV).train()
     xr = x.double().requires_grad_(True)
@@ -98,7 +98,7 @@ def test_stem_bn_relu_maxpool(shape, dtype):
         assert _rel(xg.grad, xr.grad) <= tol
         assert _rel(bn_gpu.weight.grad, bn_ref.weight.grad) <= tol
     else:
-        # bf16: ties / near-ties in the max can route the gradient to a different pixel; compare sums
+        # bf16 / fp16: ties / near-ties in the max can route the gradient to a different pixel; compare sums
         assert abs(xg.grad.float().sum().item() - xr.grad.sum().item()) <= 3e-2 * xr.grad.abs().sum().item()
     assert _rel(bn_gpu.running_mean, bn_ref.running_mean) <= 1e-6
 
@@ -113,7 +113,7 @@ def test_stem_eval_matches_torch():
     assert _rel(y, ref) <= 1e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
 @pytest.mark.parametrize("cfg", [(2, 64, 64, 15, 3, 1), (3, 64, 128, 9, 3, 2), (2, 128, 256, 7, 1, 2),
                                  (1, 256, 512, 5, 3, 1), (4, 32, 64, 33, 3, 1)],
                          ids=lambda c: "N%dC%dK%dH%dR%ds%d" % c)
@@ -145,7 +145,7 @@ def test_conv_bn_stats_fused(cfg, dtype):
     assert _rel(bn_a.running_var, bn_b.running_var) <= 1e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
 def test_stem_stats_fused(dtype):
     from sqr.bn import stem
     from sqr.conv import conv2d

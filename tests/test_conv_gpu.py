@@ -5,7 +5,8 @@ Tolerances, relative to max|ref| of each output:
   f32 (exact-f32 MFMA, the parity mode): 1e-5 (sums of up to 4608 products, f32 accumulate;
       measured <= 2.7e-6)
   bf16 inputs (f32 accumulate): y/dx rounded to bf16 -> 8e-3; dw stays f32 -> 2e-4
-  (the bf16 reference is computed from the same bf16-rounded operands).
+  fp16 inputs (f32 accumulate): y/dx rounded to fp16 (2^-11 relative) -> 1e-3; dw -> 2e-4
+  (the 16-bit reference is computed from the same rounded operands).
 """
 import pytest
 import torch
@@ -53,7 +54,7 @@ def _rel(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
 @pytest.mark.parametrize("shape", RESNET + EXTRA, ids=lambda s: "N%dC%dH%dK%dR%ds%dp%d" % s)
 def test_conv_fwd_bwd(shape, dtype):
     from sqr import conv as sc
@@ -61,15 +62,15 @@ def test_conv_fwd_bwd(shape, dtype):
     g = torch.Generator().manual_seed(N * 1000 + C * 10 + K)
     x = torch.randn(N, C, H, H, generator=g)
     w = torch.randn(K, C, R, R, generator=g) / (C * R * R) ** 0.5
-    if dtype == torch.bfloat16:
-        x = x.bfloat16().float()
-        w_used = w.bfloat16().float()
+    if dtype != torch.float32:
+        x = x.to(dtype).float()
+        w_used = w.to(dtype).float()
     else:
         w_used = w
     Ho = (H + 2 * pad - R) // st + 1
     gy = torch.randn(N, K, Ho, Ho, generator=g)
-    if dtype == torch.bfloat16:
-        gy = gy.bfloat16().float()
+    if dtype != torch.float32:
+        gy = gy.to(dtype).float()
     yr, dxr, dwr = _ref(x, w_used, st, pad, gy)
 
     xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(C >= 8)
@@ -78,7 +79,7 @@ def test_conv_fwd_bwd(shape, dtype):
     assert y.dtype == dtype and y.shape == (N, K, Ho, Ho)
     y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
     torch.cuda.synchronize()
-    tol_y = 1e-5 if dtype == torch.float32 else 8e-3
+    tol_y = {torch.float32: 1e-5, torch.bfloat16: 8e-3, torch.float16: 1e-3}[dtype]
     tol_w = 1e-5 if dtype == torch.float32 else 2e-4
     assert _rel(y, yr) <= tol_y
     assert wg.grad.dtype == torch.float32
@@ -133,25 +134,26 @@ DIRECT = [
 ]
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
 @pytest.mark.parametrize("shape", DIRECT, ids=lambda s: "N%dC%dH%dK%d" % s)
-def test_conv3_direct(shape):
+def test_conv3_direct(shape, dtype):
     from sqr import conv as sc
     from sqr._lib import lib
     N, C, H, K = shape
     g = torch.Generator().manual_seed(N + C + H + K)
-    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    x = torch.randn(N, C, H, H, generator=g).to(dtype).float()
     w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
-    gy = torch.randn(N, K, H, H, generator=g).bfloat16().float()
-    yr, dxr, dwr = _ref(x, w.bfloat16().float(), 1, 1, gy)
+    gy = torch.randn(N, K, H, H, generator=g).to(dtype).float()
+    yr, dxr, dwr = _ref(x, w.to(dtype).float(), 1, 1, gy)
     res = {}
     old = lib().sqr_conv_set_direct(2)
     try:
         for mode in (2, 0):
             lib().sqr_conv_set_direct(mode)
-            xg = x.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
             wg = w.to(DEV).requires_grad_(True)
             y, st = sc.conv2d(xg, wg, None, 1, 1, stats=True)
-            y.backward(gy.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last))
+            y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
             torch.cuda.synchronize()
             res[mode] = (y.float(), xg.grad.float(), st.double().sum(0), wg.grad.clone())
     finally:
@@ -233,3 +235,132 @@ def test_conv3s2_dgrad_direct(shape):
         x = torch.zeros(N, C, H, H)
         _, dxr, _ = _ref(x, w.bfloat16().float(), 2, 1, gy)
         assert _rel(res[1], dxr) <= 8e-3
+
+
+# ---------------------------------------------------------------------------- benchmark sizes
+# The kernels the B=64 bench step runs, at exactly its shapes, against float64 CPU references on
+# the same 16-bit-rounded operands (not only against another HIP kernel).
+
+def _f64_fwd_dgrad_wgrad(x, w, gy, stride, pad):
+    xd, wd, gd = x.double(), w.double(), gy.double()
+    y = F.conv2d(xd, wd, stride=stride, padding=pad)
+    dx = torch.nn.grad.conv2d_input(xd.shape, wd, gd, stride=stride, padding=pad)
+    dw = torch.nn.grad.conv2d_weight(xd, wd.shape, gd, stride=stride, padding=pad)
+    return y, dx, dw
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("N", [64, 48])
+def test_conv3p_bench_size_vs_f64(N, dtype):
+    """Layer-1 3x3 64->64 at the bench batch: the persistent resident-weight kernel (bands of 8+
+    tiles per workgroup, the row ring wrapping) for forward and backward-data, the direct weight
+    gradient, and the fused BatchNorm partials — all against float64."""
+    from sqr import conv as sc
+    g = torch.Generator().manual_seed(1000 + N)
+    x = torch.randn(N, 64, 64, 64, generator=g).to(dtype).float()
+    w = (torch.randn(64, 64, 3, 3, generator=g) / 24.0)
+    gy = torch.randn(N, 64, 64, 64, generator=g).to(dtype).float()
+    yr, dxr, dwr = _f64_fwd_dgrad_wgrad(x, w.to(dtype).float(), gy, 1, 1)
+    d = sc._desc(N, 64, 64, 64, 64, 3, 3, 1, 1, dtype)
+    krsc, crsk = sc.pack_weight(w.to(DEV), d, True)
+    xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    gyg = gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    y, st = sc.conv2d_fwd(xg, krsc, d, stats=True)
+    dx = sc.conv2d_bwd_data(gyg, crsk, d)
+    dw = sc.conv2d_bwd_weight(xg, gyg, d)
+    torch.cuda.synchronize()
+    assert st.shape[0] <= 256  # one partial row per persistent workgroup
+    tol = 8e-3 if dtype == torch.bfloat16 else 1e-3
+    assert _rel(y, yr) <= tol
+    assert _rel(dx, dxr) <= tol
+    assert _rel(dw, dwr) <= 2e-4
+    yd = y.double().cpu()
+    assert _rel(st.double().sum(0)[0], yd.sum((0, 2, 3))) <= 1e-5
+    assert _rel(st.double().sum(0)[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape", [(64, 64, 64, 128), (64, 128, 32, 256), (64, 256, 16, 512)],
+                         ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv3s2_dgrad_bench_size_vs_f64(shape, dtype):
+    """The direct stride-2 backward-data kernel of layers 2-4 at the bench batch vs float64."""
+    from sqr import conv as sc
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(7 * N + C + K)
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    gy = torch.randn(N, K, H // 2, H // 2, generator=g).to(dtype).float()
+    d = sc._desc(N, C, H, H, K, 3, 3, 2, 1, dtype)
+    _, crsk = sc.pack_weight(w.to(DEV), d, True)
+    dx = sc.conv2d_bwd_data(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last), crsk, d)
+    torch.cuda.synchronize()
+    dxr = torch.nn.grad.conv2d_input((N, C, H, H), w.to(dtype).double(), gy.double(), stride=2, padding=1)
+    assert _rel(dx, dxr) <= (8e-3 if dtype == torch.bfloat16 else 1e-3)
+
+
+@pytest.mark.parametrize("shape", [(64, 128, 32, 128), (64, 256, 16, 256), (64, 512, 8, 512)],
+                         ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv3_tiled_bench_size_vs_f64(shape):
+    """The tiled direct 3x3/s1 kernels of layers 2-4 (fwd + dgrad) and their weight gradient at
+    the bench batch vs float64 (bf16 operands)."""
+    from sqr import conv as sc
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(N + C + H)
+    x = torch.randn(N, C, H, H, generator=g).bfloat16().float()
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    gy = torch.randn(N, K, H, H, generator=g).bfloat16().float()
+    yr, dxr, dwr = _f64_fwd_dgrad_wgrad(x, w.bfloat16().float(), gy, 1, 1)
+    d = sc._desc(N, C, H, H, K, 3, 3, 1, 1, torch.bfloat16)
+    krsc, crsk = sc.pack_weight(w.to(DEV), d, True)
+    xg = x.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    gyg = gy.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = sc.conv2d_fwd(xg, krsc, d)
+    dx = sc.conv2d_bwd_data(gyg, crsk, d)
+    dw = sc.conv2d_bwd_weight(xg, gyg, d)
+    torch.cuda.synchronize()
+    assert _rel(y, yr) <= 8e-3 and _rel(dx, dxr) <= 8e-3 and _rel(dw, dwr) <= 2e-4
+
+
+# every conv of ResNetSQ at 512x512 input (BASELINE config 5), N=2, direct kernels forced where the
+# shape tiles (at N=2 the default routing would leave some to the implicit GEMM)
+RESNET512 = [
+    (2, 1, 512, 64, 7, 2, 3),
+    (2, 64, 128, 64, 3, 1, 1),
+    (2, 64, 128, 128, 3, 2, 1),
+    (2, 64, 128, 128, 1, 2, 0),
+    (2, 128, 64, 128, 3, 1, 1),
+    (2, 128, 64, 256, 3, 2, 1),
+    (2, 128, 64, 256, 1, 2, 0),
+    (2, 256, 32, 256, 3, 1, 1),
+    (2, 256, 32, 512, 3, 2, 1),
+    (2, 256, 32, 512, 1, 2, 0),
+    (2, 512, 16, 512, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["f16", "bf16"])
+@pytest.mark.parametrize("direct", [2, 0], ids=["direct", "gemm"])
+@pytest.mark.parametrize("shape", RESNET512, ids=lambda s: "N%dC%dH%dK%dR%ds%dp%d" % s)
+def test_conv_512(shape, direct, dtype):
+    from sqr import conv as sc
+    from sqr._lib import lib
+    N, C, H, K, R, st, pad = shape
+    g = torch.Generator().manual_seed(N * 1000 + C * 10 + K + H)
+    x = torch.randn(N, C, H, H, generator=g).to(dtype).float()
+    w = torch.randn(K, C, R, R, generator=g) / (C * R * R) ** 0.5
+    Ho = (H + 2 * pad - R) // st + 1
+    gy = torch.randn(N, K, Ho, Ho, generator=g).to(dtype).float()
+    yr, dxr, dwr = _f64_fwd_dgrad_wgrad(x, w.to(dtype).float(), gy, st, pad)
+    old = lib().sqr_conv_set_direct(direct)
+    try:
+        xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(C >= 8)
+        wg = w.to(DEV).requires_grad_(True)
+        y = sc.conv2d(xg, wg, None, st, pad)
+        y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+    finally:
+        lib().sqr_conv_set_direct(old)
+    tol = 8e-3 if dtype == torch.bfloat16 else 1e-3
+    assert _rel(y, yr) <= tol
+    assert _rel(wg.grad, dwr) <= 2e-4
+    if C >= 8:
+        assert _rel(xg.grad, dxr) <= tol

@@ -2,7 +2,7 @@
 
 Tolerances (north star): loss <= 1e-4 relative (fp32 kernel vs f64 reference).  Gradients are
 fp32 sums over R^3 voxels of a sigmoid with sharpness up to 260; they are compared with
-max|g - g_ref| <= 2e-3 * max|g_ref| per sample (measured ~1e-5-1e-4).
+max|g - g_ref| <= 2e-4 * max|g_ref| per sample (measured ~1e-5-1e-4).
 """
 import numpy as np
 import pytest
@@ -40,7 +40,7 @@ def _run_implicit(true, pred, R, tau, s, grad=True):
     return loss, (p.grad.cpu().numpy() if grad else None)
 
 
-def _grad_close(g, gref, rel=2e-3):
+def _grad_close(g, gref, rel=2e-4):
     for b in range(g.shape[0]):
         scale = max(np.abs(gref[b]).max(), 1e-12)
         assert np.abs(g[b] - gref[b]).max() <= rel * scale, (b, g[b], gref[b])
@@ -165,3 +165,64 @@ def test_iou_vs_golden(case):
     cnt = O.iou_counts(case["true"], case["pred"], R)
     from sqr import losses
     assert np.array_equal(losses.iou_counts(t, p, R).cpu().numpy(), cnt)
+
+
+# ---------------------------------------------------------------------------- config 4
+def test_combined_explicit_implicit_vs_oracle():
+    """BASELINE config 4 (the torch/visu.py path): ExplicitLoss(32)(p_true, pred) +
+    ImplicitLoss(64, tau 1.5, s 260)(image, pred) through one backward vs the f64 oracle."""
+    from sqr import losses
+    C = _classes()
+    rng = np.random.default_rng(44)
+    B = 4
+    pt, pr = _sample(rng, B), _sample(rng, B)
+    img = losses.implicit_render(torch.tensor(pt, device=DEV), 256, 1.5, 260).unsqueeze(1)
+    Le, Ge, _ = O.explicit_loss(pt, pr, 32)
+    Li, Gi, _, _ = O.implicit_loss(img.cpu().numpy(), pr, 64, 1.5, 260)
+    p = torch.tensor(pr, device=DEV, requires_grad=True)
+    loss = C.ExplicitLoss(32, DEV)(torch.tensor(pt, device=DEV), p) + C.ImplicitLoss(64, DEV, 1.5, 260)(img, p)
+    loss.backward()
+    assert loss.dtype == torch.float64
+    assert abs(loss.item() - (Le + Li)) <= 1e-4 * abs(Le + Li)
+    _grad_close(p.grad.cpu().numpy(), Ge + Gi)
+
+
+def test_combined_loss_bench_batch_properties():
+    """Config 4 at the bench batch (B=64): the combined gradient is the sum of the two losses'
+    gradients (linearity of backward), and the batch-mean splits over chunks exactly."""
+    from sqr import losses
+    C = _classes()
+    rng = np.random.default_rng(45)
+    B = 64
+    pt = torch.tensor(_sample(rng, B), device=DEV)
+    pr = _sample(rng, B)
+    img = losses.implicit_render(pt, 256, 1.5, 260).unsqueeze(1)
+    ex, im = C.ExplicitLoss(32, DEV), C.ImplicitLoss(64, DEV, 1.5, 260)
+    grads, vals = [], []
+    for parts in (("e",), ("i",), ("e", "i")):
+        p = torch.tensor(pr, device=DEV, requires_grad=True)
+        loss = sum(ex(pt, p) if k == "e" else im(img, p) for k in parts)
+        loss.backward()
+        grads.append(p.grad.clone())
+        vals.append(loss.item())
+    assert abs(vals[2] - (vals[0] + vals[1])) <= 1e-12 * abs(vals[2])
+    torch.testing.assert_close(grads[2], grads[0] + grads[1], rtol=1e-6, atol=1e-12)
+    chunks = [ex(pt[i:i + 16], torch.tensor(pr[i:i + 16], device=DEV)).item() for i in range(0, B, 16)]
+    assert abs(np.mean(chunks) - vals[0]) <= 1e-12
+    assert np.isfinite(grads[2].cpu().numpy()).all() and grads[2].abs().sum() > 0
+
+
+def test_iou_float64_params_exact_counts():
+    """visu.py feeds float64 parameters to IoUAccuracy (visu.py:142-159): they are used without
+    rounding to fp32, so the integer counts equal the f64 oracle's exactly; rounding the same
+    parameters to fp32 moves boundary voxels."""
+    from sqr import losses
+    rng = np.random.default_rng(46)
+    B, R = 48, 128
+    t = _sample(rng, B).astype(np.float64) + rng.uniform(-1e-7, 1e-7, (B, 12))
+    p = _sample(rng, B).astype(np.float64) + rng.uniform(-1e-7, 1e-7, (B, 12))
+    cnt = losses.iou_counts(torch.tensor(t, device=DEV), torch.tensor(p, device=DEV), R).cpu().numpy()
+    np.testing.assert_array_equal(cnt, O.iou_counts(t, p, R))
+    C = _classes()
+    acc = C.IoUAccuracy(R, DEV)(torch.tensor(t, device=DEV), torch.tensor(p, device=DEV))
+    assert acc.item() == pytest.approx(O.iou_accuracy(t, p, R), rel=1e-6)

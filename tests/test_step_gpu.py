@@ -1,0 +1,115 @@
+"""The benchmarked training step itself (bench.Trainer: B=64, whole step in one HIP graph, fused
+stem / tail / BatchNorm, direct convs, fused loss, fused Adam) against float64.
+
+One replay of the captured graph computes every parameter gradient of ResNetSQ + ImplicitLoss(32)
+from the weights the graph starts from.  The float64 CPU reference (oracle/ref_torch.py, the
+reference's architecture with torchvision-identical keys, reference-style f64 loss) runs the same
+step on the same images and the same 16-bit-rounded conv weights.  The tolerance is derived, not
+guessed: a CPU float32 run that rounds to the compute dtype at the GPU step's storage points (conv
+operands and outputs, BatchNorm / pooled activations, and - through autograd of the casts - the
+activation gradients) measures how far a correct 16-bit step lands from float64; the GPU step must
+land as close (x3, with a small absolute floor for parameters whose gradient is ~0).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _round16(dt):
+    def hook(_m, _inp, out):
+        return out.to(dt).float()
+    return hook
+
+
+def _emulated(ref, dt):
+    """ref_torch model (float32) whose activations are rounded to dt where the GPU step stores them."""
+    hooks = []
+    for m in ref.modules():
+        if isinstance(m, (nn.Conv2d, nn.BatchNorm2d, nn.MaxPool2d, nn.ReLU)):
+            hooks.append(m.register_forward_hook(_round16(dt)))
+    return hooks
+
+
+def _rel_err(a, b):
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("config,batch", [(2, 64), (4, 64), (5, 4)],
+                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B4"])
+def test_bench_step_gradients_vs_f64(config, batch):
+    import bench
+    import ref_torch
+    tr = bench.Trainer(torch.device(DEV), config=config, batch=batch)
+    dt = tr.dtype
+    tr.capture()
+    assert tr.graph is not None
+    # the weights this replay starts from (the capture ran 3 eager steps before), and the loss scale
+    # it runs with (fp16: gradients come out multiplied by it)
+    sd = {k: v.detach().cpu().clone() for k, v in tr.net.state_dict().items()}
+    scale = tr.scaler.get_scale() if tr.scaler is not None else 1.0
+    tr.graph.replay()
+    torch.cuda.synchronize()
+    g_gpu = {n: p.grad.detach().double().cpu() / scale for n, p in tr.net.named_parameters()}
+    loss_gpu = tr.static_loss.item()
+    images = tr.images.detach().cpu()
+
+    # conv weights as the GPU step used them (16-bit packed copies of the fp32 masters)
+    sd16 = {k: (v.to(dt).float() if (k.endswith("weight") and v.dim() == 4) else v) for k, v in sd.items()}
+
+    labels = tr.params.detach().cpu()
+
+    def run(model, x, scale=1.0):
+        pred = torch.cat(model(x), 1)
+        loss = ref_torch.ImplicitLossRef(tr.R, 1.5, 260)(images.double(), pred)
+        if tr.crit_x is not None:  # config 4: + ExplicitLoss(32) on the labels
+            loss = loss + ref_torch.ExplicitLossRef(32)(labels, pred)
+        (loss * scale).backward()
+        return loss.item(), {n: p.grad.detach().double() / scale for n, p in model.named_parameters()}
+
+    ref64 = ref_torch.ResNetSQRef().double()
+    ref64.load_state_dict(sd16)
+    loss64, g64 = run(ref64, images.double())
+    emu = ref_torch.ResNetSQRef()
+    emu.load_state_dict(sd16)
+    hooks = _emulated(emu, dt)
+    loss_emu, g_emu = run(emu, images.to(dt).float(), scale)
+    for h in hooks:
+        h.remove()
+
+    assert abs(loss_gpu - loss64) <= max(3 * abs(loss_emu - loss64), 1e-4 * abs(loss64)), (loss_gpu, loss_emu, loss64)
+    worst = []
+    for n, b in g64.items():
+        e_gpu = _rel_err(g_gpu[n], b)
+        e_emu = _rel_err(g_emu[n], b)
+        worst.append((e_gpu / max(e_emu, 1e-4), n, e_gpu, e_emu))
+        assert e_gpu <= 3 * e_emu + 1e-3, (n, e_gpu, e_emu)
+    worst.sort(reverse=True)
+    print("worst gpu/emulated error ratios:", ["%s %.2e/%.2e" % (n, a, b) for _, n, a, b in worst[:5]])
+    # the step then applied Adam: every parameter moved, by at most ~lr (Adam's first-order bound)
+    for n, p in tr.net.named_parameters():
+        delta = (p.detach().cpu() - sd[n]).abs().max().item()
+        assert 0 < delta <= 1.5e-4, (n, delta)
+
+
+@pytest.mark.timeout(300)
+def test_bench_step_graph_equals_eager():
+    """Replaying the captured step == running the same step eagerly (bitwise: every kernel is
+    deterministic), starting from identical states."""
+    import bench
+    a = bench.Trainer(torch.device(DEV), config=2, batch=16)
+    b = bench.Trainer(torch.device(DEV), config=2, batch=16, graph=False)
+    a.capture()
+    b.capture()  # no-op (graph=False)
+    for _ in range(3):  # a's capture ran 3 eager steps
+        b.step()
+    la, lb = a.step(), b.step()
+    torch.cuda.synchronize()
+    assert la.item() == lb.item()
+    for (n, p), q in zip(a.net.named_parameters(), b.net.parameters()):
+        assert torch.equal(p, q), n
+        assert torch.equal(p.grad, q.grad), n

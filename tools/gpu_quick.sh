@@ -10,8 +10,9 @@ export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 if [ "$TESTS" != "none" ]; then
-  timeout -k 10 500 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
-  tail -2 "$OUT/pytest_gpu.log"
+  timeout -k 10 ${PYTEST_LIMIT:-900} python -u -m pytest $TESTS -m gpu -q -rf --maxfail=40 --timeout 600 \
+    --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -60 "$OUT/pytest_gpu.log"; exit 1; }
+  tail -3 "$OUT/pytest_gpu.log"
 fi
 timeout -k 10 300 python -u bench.py --cpu-steps 0 > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
