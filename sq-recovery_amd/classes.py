@@ -9,8 +9,10 @@ metric math runs as fused HIP kernels on MI355X (libsqr, include/sqr.h):
   H5Dataset     classes.py:22-93   (data boundary, not accelerated; h5py imported lazily)
   QuaternionLoss, LeastSquares     (not on the hot path; plain torch)
 
-Losses take CUDA tensors; the kernels are the only implementation (no CPU fallback) — a CPU
-tensor raises ValueError.
+CUDA tensors run on the kernels only (a missing libsqr raises; nothing falls back).  CPU tensors —
+the reference's CPU configuration (BASELINE config 1) — run the float64 host implementation in
+sqr/cpu.py (batched restatement of the same math, pinned to the reference's fixtures); mixing
+devices raises.
 """
 import glob
 import os
@@ -21,7 +23,16 @@ import torch.nn.functional as F
 from torch.utils import data
 
 from quaternion import conjugate, mat_from_quaternion
+from sqr import cpu as _cpu
 from sqr import losses as _L
+
+
+def _on_cpu(*ts):
+    """True when every tensor is on the CPU (host path), False when all are on the GPU."""
+    devs = {t.is_cuda for t in ts}
+    if len(devs) > 1:
+        raise ValueError("loss inputs on different devices: %s" % ", ".join(str(t.device) for t in ts))
+    return not devs.pop()
 
 
 def _grid(axis, device):
@@ -115,10 +126,12 @@ def sample_sq_params(rng, n):
 
 
 class SyntheticDataset(data.Dataset):
-    """H5Dataset stand-in without files: n random SQs (sample_sq_params) rendered on the GPU into
-    size x size depth images in [0, 1] with the implicit-loss renderer (tau 1.5, sharpness 260),
-    held in HBM.  Same interface (set_mode / __len__ / __getitem__ -> (X [1,H,W], y [12]));
-    items are device tensors, so use a DataLoader with num_workers=0 (or batches()).
+    """H5Dataset stand-in without files: n random SQs (sample_sq_params) rendered into size x size
+    depth images in [0, 1] with the implicit-loss renderer (tau 1.5, sharpness 260), held on
+    `device` (GPU: rendered at full size by the HIP kernel, in HBM; CPU: rendered at
+    min(size, 64)^2 by the host renderer and nearest-upsampled — plumbing data for config 1).
+    Same interface (set_mode / __len__ / __getitem__ -> (X [1,H,W], y [12])); items are device
+    tensors, so use a DataLoader with num_workers=0 (or batches()).
     Rank r of a data-parallel job passes seed + r to get its own shard."""
 
     def __init__(self, n, device, train_split=0.9, size=256, seed=0, tau=1.5, sharpness=260):
@@ -126,7 +139,11 @@ class SyntheticDataset(data.Dataset):
         self.labels = torch.tensor(sample_sq_params(rng, n), device=device)
         self.images = torch.empty((n, 1, size, size), dtype=torch.float32, device=device)
         for i in range(0, n, 256):  # bounded render batches
-            self.images[i:i + 256, 0] = _L.implicit_render(self.labels[i:i + 256], size, tau, sharpness)
+            if self.labels.is_cuda:
+                self.images[i:i + 256, 0] = _L.implicit_render(self.labels[i:i + 256], size, tau, sharpness)
+            else:
+                r = _cpu.render(self.labels[i:i + 256], min(size, 64), tau, sharpness).float().unsqueeze(1)
+                self.images[i:i + 256] = F.interpolate(r, size=(size, size), mode="nearest")
         self.n_train = int(train_split * n)
         self.n_val = n - self.n_train
         self.mode = 0
@@ -188,6 +205,8 @@ class ExplicitLoss:
     preprocess_sq = staticmethod(_preprocess_sq)
 
     def __call__(self, true, pred):
+        if _on_cpu(true, pred):
+            return _cpu.explicit_loss(true, pred, self.render_size)
         return _L.explicit_loss(true, pred, self.render_size)
 
 
@@ -215,10 +234,14 @@ class ImplicitLoss:
     preprocess_sq = staticmethod(_preprocess_sq)
 
     def depth_projection(self, p):
-        """classes.py:232-282: [B,12] -> [B,R,R] depth renders (HIP kernel; no autograd)."""
+        """classes.py:232-282: [B,12] -> [B,R,R] depth renders (HIP kernel; no autograd on the GPU)."""
+        if _on_cpu(p):
+            return _cpu.render(p, self.render_size, self.tau, self.sigmoid_sharpness)
         return _L.implicit_render(p, self.render_size, self.tau, self.sigmoid_sharpness).to(torch.float64)
 
     def __call__(self, true, pred):
+        if _on_cpu(true, pred):
+            return _cpu.implicit_loss(true, pred, self.render_size, self.tau, self.sigmoid_sharpness)
         return _L.implicit_loss(true, pred, self.render_size, self.tau, self.sigmoid_sharpness)
 
 
@@ -236,7 +259,10 @@ class IoUAccuracy:
         self.full = full
 
     def __call__(self, true, pred):
-        cnt = _L.iou_counts(true, pred, self.render_size)
+        if _on_cpu(true, pred):
+            cnt = _cpu.iou_counts(true, pred, self.render_size)
+        else:
+            cnt = _L.iou_counts(true, pred, self.render_size)
         if not self.reduce:
             return cnt[:, 0].double() / cnt[:, 1].double()
         tot = cnt.sum(0)

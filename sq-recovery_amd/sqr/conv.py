@@ -330,11 +330,13 @@ class Conv2d(nn.Conv2d):
         return None
 
     def forward(self, x):
+        if not x.is_cuda:  # CPU tensors (BASELINE config 1): torch's own CPU convolution
+            return super().forward(x)
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x))
 
     def forward_stats(self, x, bn=None):
         """(y, BatchNorm partials of y) — see conv2d(stats=True).  With `bn` given, the partials
         are produced only when that BatchNorm will use batch statistics (else y alone)."""
-        if bn is not None and not (bn.training or not bn.track_running_stats):
+        if not x.is_cuda or (bn is not None and not (bn.training or not bn.track_running_stats)):
             return self.forward(x)
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x), stats=True)

@@ -1,10 +1,11 @@
 """Data-parallel plumbing shared by train.py and bench.py.
 
 One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE), backend
-"nccl" = RCCL over xGMI on ROCm.  Images are independent, so the only data-path collective is the
-gradient all-reduce that DistributedDataParallel buckets and overlaps with backward; BatchNorm keeps
-per-rank batch statistics (the reference trains on one GPU; DDP without SyncBN is the documented
-multi-GPU semantics: an N-rank step equals the average of N independent per-rank gradients).
+"nccl" = RCCL over xGMI on ROCm (gloo for CPU runs).  Images are independent, so the only data-path
+collective is the gradient all-reduce, bucketed and overlapped with backward by GraphDataParallel
+(below); BatchNorm keeps per-rank batch statistics (the reference trains on one GPU; DDP without
+SyncBN is the documented multi-GPU semantics: an N-rank step equals the average of N independent
+per-rank gradients).  ``wrap`` (torch DDP) remains as the fallback when a step cannot be captured.
 """
 import os
 
@@ -65,17 +66,20 @@ def wrap(model, device):
 class GraphDataParallel:
     """Data parallelism whose whole step — forward, loss, backward, gradient all-reduce, optimizer —
     can be captured as ONE HIP graph (DDP's reducer cannot be captured, and eager launching of the
-    ~200-kernel step is host-bound).
+    ~200-kernel step is host-bound).  Used by bench.py (captured) and train.py (eager) alike.
 
-    Every parameter gradient of a libsqr model (ResNetSQ: convs, BatchNorm, stem, tail) is written by
-    its backward op straight into a slot of one flat fp32 buffer (sqr.gradbuf, in backward order).
-    The buffer is cut into buckets of ~``bucket_mb``; as soon as the backward has enqueued the last
-    gradient of a bucket, that bucket is summed in place over the ranks by RCCL on a side stream,
-    overlapping the rest of the backward (the dependencies are stream events, so they are captured
-    with the graph).  ``allreduce()`` (after ``backward``) joins the side stream; the fused optimizer
-    averages while it reads (``optimizer.sqr_grad_scale = 1 / world``).  Semantics are DDP's:
-    parameters and buffers are broadcast from rank 0 once, BatchNorm statistics stay per rank.
-    Gradients must be None before each backward (``zero_grad(set_to_none=True)``)."""
+    Every parameter gradient lives in a slot of one flat fp32 buffer (sqr.gradbuf, in backward
+    order): libsqr's backward ops (ResNetSQ: convs, BatchNorm, stem, tail) write their weight
+    gradients straight into the slots; any other op's gradient is moved into its slot by the
+    parameter's post-accumulate-grad hook (the host CPU path, plain torch modules).  The buffer is
+    cut into buckets of ~``bucket_mb``; as soon as the backward has produced the last gradient of a
+    bucket, that bucket is summed in place over the ranks (RCCL on a side stream for CUDA,
+    overlapping the rest of the backward; the dependencies are stream events, so they are captured
+    with the graph; gloo in-line on the CPU).  ``allreduce()`` (after ``backward``) joins the side
+    stream; the fused optimizer averages while it reads (``optimizer.sqr_grad_scale = 1 / world``;
+    other optimizers get the buffer scaled once).  Semantics are DDP's: parameters and buffers are
+    broadcast from rank 0 once, BatchNorm statistics stay per rank.  Gradients must be None before
+    each backward (``optimizer.zero_grad(set_to_none=True)``; checked)."""
 
     def __init__(self, model, optimizer, device, bucket_mb=BUCKET_MB):
         from . import gradbuf
@@ -88,8 +92,9 @@ class GraphDataParallel:
                     dist.broadcast(t.data, 0)
         order = list(reversed(self.params))  # the backward produces the last layers' grads first
         self.flat = gradbuf.install(order, device)
+        self.param_of = {id(p): p for p in self.params}
         # buckets: contiguous ranges of the flat buffer
-        self.buckets, self.bucket_of, size, start, members = [], {}, 0, 0, []
+        self.buckets, self.bucket_of, start, members = [], {}, 0, []
         cap = int(bucket_mb * 2 ** 20 / 4)
         off = 0
         for p in order:
@@ -105,19 +110,28 @@ class GraphDataParallel:
                 self.bucket_of[pid] = b
         device = torch.device(device)
         self.side = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self.launch_log = []  # bucket indices in launch order (tests)
         self._reset()
         gradbuf.set_listener(self._written)
-        optimizer.sqr_grad_scale = 1.0 / self.world
+        self._hooks = [p.register_post_accumulate_grad_hook(self._accumulated) for p in self.params]
+        self._hooks.append(model.register_forward_pre_hook(self._check_cleared))
+        # the fused CUDA optimizer averages while it reads; otherwise the buffer is scaled once
+        self.fused_scale = hasattr(optimizer, "sqr_grad_scale") and device.type == "cuda"
+        if self.fused_scale:
+            optimizer.sqr_grad_scale = 1.0 / self.world
 
     def _reset(self):
         self.pending = [len(mem) for _, _, mem in self.buckets]
         self.launched = [False] * len(self.buckets)
+        self.done = set()
 
     def _launch(self, b):
-        if self.launched[b] or not dist.is_initialized():
-            self.launched[b] = True
+        if self.launched[b]:
             return
         self.launched[b] = True
+        self.launch_log.append(b)
+        if not dist.is_initialized():
+            return
         lo, hi, _ = self.buckets[b]
         view = self.flat[lo:hi]
         if self.side is None:
@@ -127,14 +141,47 @@ class GraphDataParallel:
         with torch.cuda.stream(self.side):
             dist.all_reduce(view)  # SUM in place; the optimizer scales by 1 / world
 
+    def _mark(self, pid):
+        if pid in self.done:
+            return
+        self.done.add(pid)
+        b = self.bucket_of.get(pid)
+        if b is None:
+            return
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def _check_cleared(self, _module, _inputs):
+        """forward pre-hook: a gradient-recording forward must start with every gradient None, or
+        the backward would add into the previous step's flat-buffer slots."""
+        if torch.is_grad_enabled() and any(p.grad is not None for p in self.params):
+            raise RuntimeError("GraphDataParallel: parameter gradients were not cleared before the forward "
+                               "(use optimizer.zero_grad(set_to_none=True))")
+
     def _written(self, pids):
+        """sqr.gradbuf listener: a libsqr backward op has enqueued these parameters' gradients
+        into their slots (AccumulateGrad will adopt the slot views as p.grad)."""
         for pid in pids:
-            b = self.bucket_of.get(pid)
-            if b is None:
+            p = self.param_of.get(pid)
+            if p is None:
                 continue
-            self.pending[b] -= 1
-            if self.pending[b] == 0:
-                self._launch(b)
+            if p.grad is not None:
+                raise RuntimeError("GraphDataParallel: a parameter gradient was not cleared before backward "
+                                   "(use optimizer.zero_grad(set_to_none=True)); the slot would be added to itself")
+            self._mark(pid)
+
+    def _accumulated(self, p):
+        """post-accumulate-grad hook: gradients produced by other ops are moved into their slot."""
+        from . import gradbuf
+        pid = id(p)
+        slot = gradbuf.out(pid, tuple(p.shape), p.device)
+        if p.grad.data_ptr() != slot.data_ptr():
+            if pid in self.done:
+                raise RuntimeError("GraphDataParallel: parameter gradient accumulated twice in one backward")
+            slot.copy_(p.grad)
+            p.grad = slot
+        self._mark(pid)
 
     def allreduce(self):
         """Finish the gradient all-reduce of this step (call after backward, before the optimizer)."""
@@ -142,6 +189,8 @@ class GraphDataParallel:
             self._launch(b)  # buckets whose gradients were not all produced
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
+        if not self.fused_scale and self.world > 1:
+            self.flat.mul_(1.0 / self.world)
         self._reset()
 
     def check_grads(self):
@@ -150,12 +199,14 @@ class GraphDataParallel:
         hi = lo + self.flat.numel() * self.flat.element_size()
         for p in self.params:
             if p.grad is None or not lo <= p.grad.data_ptr() < hi:
-                raise RuntimeError("GraphDataParallel: a parameter gradient was not produced by a libsqr op")
+                raise RuntimeError("GraphDataParallel: a parameter gradient is not in the flat buffer")
 
     def close(self, optimizer=None):
         from . import gradbuf
         gradbuf.clear()
-        if optimizer is not None:
+        for h in self._hooks:
+            h.remove()
+        if optimizer is not None and hasattr(optimizer, "sqr_grad_scale"):
             optimizer.sqr_grad_scale = 1.0
 
 

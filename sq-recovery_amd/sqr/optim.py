@@ -23,10 +23,13 @@ class Adam(torch.optim.Adam):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, **kw):
         for k in ("fused", "foreach", "capturable"):
             kw.pop(k, None)
+        params = list(params)
+        flat = [q for g in params for q in (g["params"] if isinstance(g, dict) else [g])]
         # capturable: per-parameter step counters live on the device (graph-capturable, and the
-        # state layout torch.optim.Adam(capturable=True) uses)
+        # state layout torch.optim.Adam(capturable=True) uses); CPU parameters (config 1) use
+        # torch's own CPU step
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad,
-                         capturable=True, **kw)
+                         capturable=all(q.is_cuda for q in flat), **kw)
         self._convs = {}  # id(weight) -> (module, dtype)
         # gradients are read as g * grad_scale (sqr.dist.GraphDataParallel sets 1/world after a SUM
         # all-reduce; the fallback path requires 1)

@@ -30,6 +30,10 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        if not x.is_cuda:  # CPU tensors (BASELINE config 1): torchvision's BasicBlock composition
+            identity = x if self.downsample is None else self.downsample(x)
+            out = self.bn2(self.conv2(self.relu(self.bn1(self.conv1(x)))))
+            return self.relu(out + identity)
         # conv -> fused [bn+relu] -> conv -> fused [bn + identity + relu]   (libsqr kernels)
         # (training: each conv's epilogue also emits the batch statistics its BN needs)
         out = bn_act(self.conv1.forward_stats(x, self.bn1), self.bn1, relu=True, counted=True)
@@ -74,6 +78,9 @@ class ResNet18(nn.Module):
 
     def features(self, x):
         """conv1 .. layer4: the NHWC layer-4 activation (before average pooling)."""
+        if not x.is_cuda:  # CPU tensors: torchvision's stem
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+            return self.layer4(self.layer3(self.layer2(self.layer1(x))))
         convs = [m for m in self.modules() if isinstance(m, Conv2d)]
         # bf16: conv1 + bn1 + relu + maxpool as one op that never writes the conv1 activation
         fuse = x.is_cuda and compute_dtype(x) == torch.bfloat16 and fused_stem_ok(x, self.conv1, self.bn1)

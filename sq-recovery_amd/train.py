@@ -1,18 +1,25 @@
 """Drop-in for torch/train.py (timoblak/sq-recovery) on MI355X.
 
 Same loop as the reference (train.py:72-175): per batch zero_grad -> ResNetSQ forward ->
-cat(a, e, t, q) -> ImplicitLoss(R, tau 1.5, s 260)(images, pred) -> backward -> Adam(1e-4) step ->
-loss.item(); NaN check on encoder.fc[0].weight.grad; per epoch a validation pass with the loss and
-IoUAccuracy(64, full=True), ReduceLROnPlateau(patience 25) on the validation loss, checkpoint
-(helpers.save_model format) whenever the validation loss improves.
+cat(a, e, t, q) -> loss -> backward -> Adam(1e-4) step -> loss.item(); NaN check on
+encoder.fc[0].weight.grad; per epoch a validation pass with the loss and IoUAccuracy(64, full=True),
+ReduceLROnPlateau(patience 25) on the validation loss, checkpoint (helpers.save_model format)
+whenever the validation loss improves.  The loss is the reference's choice (train.py:62-64):
+--loss implicit (default: ImplicitLoss(R, tau 1.5, s 260)(images, pred)), explicit
+(ExplicitLoss(R)(labels, pred)) or combined (their sum, the visu.py pairing).
 
 MI355X-specific:
-  * convs / BatchNorm / losses run on the libsqr HIP kernels (no CPU fallback);
-  * --bf16 runs the network under bf16 autocast (the loss kernel always consumes fp32 params);
+  * on CUDA the convs / BatchNorm / losses run on the libsqr HIP kernels (nothing falls back);
+    --device cpu runs the reference's CPU configuration (BASELINE config 1) on torch's CPU ops and
+    the float64 host losses (sqr/cpu.py);
+  * --bf16 / --fp16 run the network under autocast (fp16 with sqr.amp.GradScaler loss scaling); the
+    loss kernels always consume fp32 params;
   * data parallel: launch with `torchrun --nproc-per-node 8 train.py ...` — one process per GPU,
-    DDP gradient all-reduce over RCCL, each rank trains on its own contiguous shard
-    (sqr.dist.shard), rank 0 logs and writes checkpoints (un-prefixed state-dict keys);
-  * --synthetic N trains on N GPU-rendered SQ images (no dataset files needed); otherwise the
+    sqr.dist.GraphDataParallel (the same bucketed RCCL all-reduce, overlapped with backward, that
+    bench.py captures in its step graph; run eagerly here because the loop reads the loss every
+    step), each rank trains on its own contiguous shard (sqr.dist.shard), rank 0 logs and writes
+    checkpoints (un-prefixed state-dict keys);
+  * --synthetic N trains on N rendered SQ images (no dataset files needed); otherwise the
     reference's H5Dataset(dataset_location, parse_csv(labels), 0.9) is used (needs h5py).
 """
 import argparse
@@ -26,10 +33,10 @@ import torch.utils.data as data
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from classes import H5Dataset, ImplicitLoss, IoUAccuracy, SyntheticDataset  # noqa: E402
+from classes import ExplicitLoss, H5Dataset, ImplicitLoss, IoUAccuracy, SyntheticDataset  # noqa: E402
 from helpers import load_model, parse_csv, save_compare_images, save_model  # noqa: E402
 from models import ResNetSQ  # noqa: E402
-from sqr import dist  # noqa: E402
+from sqr import amp, dist  # noqa: E402
 from sqr.optim import Adam  # noqa: E402
 
 
@@ -42,12 +49,17 @@ def parse_args(argv=None):
     ap.add_argument("--epochs", type=int, default=20000)
     ap.add_argument("--batch-size", type=int, default=32, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=1e-4)
-    ap.add_argument("--render-size", type=int, default=64)
+    ap.add_argument("--render-size", type=int, default=64, help="ImplicitLoss render size (train.py:64)")
+    ap.add_argument("--explicit-render-size", type=int, default=32, help="ExplicitLoss render size (train.py:62)")
     ap.add_argument("--log-interval", type=int, default=1)
     ap.add_argument("--running-mean", type=int, default=100)
     ap.add_argument("--pretrained", type=int, default=1)
     ap.add_argument("--continue-training", action="store_true")
     ap.add_argument("--bf16", action="store_true", help="bf16 autocast for the network")
+    ap.add_argument("--fp16", action="store_true", help="fp16 autocast + dynamic loss scaling")
+    ap.add_argument("--loss", default="implicit", choices=("implicit", "explicit", "combined"),
+                    help="training loss (reference train.py:62-64)")
+    ap.add_argument("--device", default="auto", choices=("auto", "cuda", "cpu"))
     ap.add_argument("--compare-images", action="store_true",
                     help="render val batch 0 with the external scanner (helpers.save_compare_images)")
     ap.add_argument("--max-steps", type=int, default=0, help="stop an epoch after this many steps (0 = all)")
@@ -55,12 +67,14 @@ def parse_args(argv=None):
 
 
 def _batches(dataset, rank, world, batch_size):
-    """This rank's batches of the current split (contiguous shard, no shuffle, like the reference)."""
+    """This rank's batches of the current split (contiguous shard, no shuffle, like the reference;
+    the last batch may be partial, as with the reference's DataLoader)."""
     idx = dist.shard(len(dataset), rank, world)
     if isinstance(dataset, SyntheticDataset):
         off = 0 if dataset.mode == 0 else dataset.n_train
-        for i in range(idx.start, idx.stop - batch_size + 1, batch_size):
-            yield (dataset.images[off + i:off + i + batch_size], dataset.labels[off + i:off + i + batch_size])
+        for i in range(idx.start, idx.stop, batch_size):
+            j = min(i + batch_size, idx.stop)
+            yield (dataset.images[off + i:off + j], dataset.labels[off + i:off + j])
         return
     loader = data.DataLoader(data.Subset(dataset, list(idx)), batch_size=batch_size, shuffle=False, num_workers=4)
     yield from loader
@@ -68,7 +82,8 @@ def _batches(dataset, rank, world, batch_size):
 
 def main(argv=None):
     args = parse_args(argv)
-    rank, world, device = dist.init("nccl")
+    use_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
+    rank, world, device = dist.init("nccl" if use_cuda else "gloo")
     main_rank = rank == 0
     if main_rank:
         print("Using device: %s (world size %d)" % (device, world))
@@ -80,23 +95,37 @@ def main(argv=None):
         dataset = H5Dataset(args.dataset_location, parse_csv(args.labels), train_split=0.9, dataset_file="dataset.h5")
 
     net = ResNetSQ(outputs=4, pretrained=bool(args.pretrained)).to(device)
-    # torch.optim.Adam semantics / state_dict on libsqr's fused step (+ bf16 conv weight packing)
+    # torch.optim.Adam semantics / state_dict on libsqr's fused step (+ 16-bit conv weight packing)
     optimizer = Adam(net.parameters(), lr=args.lr, weight_decay=0)
-    if args.bf16:
-        optimizer.attach(net)
+    amp_dtype = torch.bfloat16 if args.bf16 else (torch.float16 if args.fp16 else None)
+    if amp_dtype is not None and use_cuda:
+        optimizer.attach(net, amp_dtype)
+    scaler = amp.GradScaler(device) if (args.fp16 and use_cuda) else None
     scheduler = optim.lr_scheduler.ReduceLROnPlateau(optimizer, patience=25)
     starting_epoch = 0
     if args.continue_training:
         if main_rank:
             print("Continuing with training...")
         starting_epoch, net, optimizer, _ = load_model(args.model_location, net, optimizer)
-    model = dist.wrap(net, device)
+    # N > 1: bucketed gradient all-reduce overlapped with backward (the same machinery bench.py
+    # captures in its step graph); the model itself stays unwrapped (checkpoints keep plain keys)
+    gdp = dist.GraphDataParallel(net, optimizer, device) if world > 1 else None
+    model = net
 
-    loss_criterion = ImplicitLoss(args.render_size, device, 1.5, 260)
+    implicit = ImplicitLoss(args.render_size, device, 1.5, 260)
+    explicit = ExplicitLoss(args.explicit_render_size, device)
+
+    def loss_criterion(images, labels, pred):
+        if args.loss == "implicit":
+            return implicit(images, pred)
+        if args.loss == "explicit":
+            return explicit(labels, pred)
+        return explicit(labels, pred) + implicit(images, pred)
+
     accuracy_estimator = IoUAccuracy(render_size=64, device=device, full=True)
 
     def forward(x):
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=args.bf16):
+        with torch.autocast("cuda", dtype=amp_dtype or torch.bfloat16, enabled=amp_dtype is not None and use_cuda):
             out = model(x)
         return torch.cat([o.float() for o in out], dim=1)
 
@@ -111,11 +140,17 @@ def main(argv=None):
             if args.max_steps and batch_idx >= args.max_steps:
                 break
             x, true_labels = x.to(device, non_blocking=True), true_labels.to(device, non_blocking=True)
-            optimizer.zero_grad()
+            optimizer.zero_grad(set_to_none=True)
             pred_labels = forward(x)
-            loss = loss_criterion(x, pred_labels)
-            loss.backward()
-            optimizer.step()
+            loss = loss_criterion(x, true_labels, pred_labels)
+            (scaler.scale(loss) if scaler is not None else loss).backward()
+            if gdp is not None:
+                gdp.allreduce()
+            if scaler is not None:
+                scaler.step(optimizer)
+                scaler.update()
+            else:
+                optimizer.step()
             losses.append(loss.item())
             if torch.any(torch.isnan(net.encoder.fc[0].weight.grad)):
                 print("--------------- NAN GRADS!!!! ---------------")
@@ -139,7 +174,7 @@ def main(argv=None):
                     break
                 x, true_labels = x.to(device), true_labels.to(device)
                 pred_labels = forward(x)
-                loss = loss_criterion(x, pred_labels)
+                loss = loss_criterion(x, true_labels, pred_labels)
                 acc = accuracy_estimator(true_labels, pred_labels)
                 if batch_idx == 0 and main_rank and args.compare_images:
                     save_compare_images(true_labels.cpu().numpy(), pred_labels.cpu().numpy())
@@ -164,6 +199,8 @@ def main(argv=None):
             print("=" * 72)
         else:
             best_val_loss = val_loss_mean if best_val_loss is None else min(best_val_loss, val_loss_mean)
+    if gdp is not None:
+        gdp.close(optimizer)
     dist.finish()
     return mean_losses, mean_val_losses
 

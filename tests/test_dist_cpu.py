@@ -6,12 +6,19 @@
   gradient_as_bucket_view, no buffer broadcast) equals the average of the per-rank independent
   gradients — the documented N-GPU semantics (per-rank BatchNorm statistics) — checked on the
   oracle's CPU ResNetSQ (the HIP model needs a GPU; the DDP wiring is model-agnostic);
-* helpers.save_model on the DDP-wrapped model writes un-prefixed keys that load into a bare model.
+* helpers.save_model on the DDP-wrapped model writes un-prefixed keys that load into a bare model;
+* sqr.dist.GraphDataParallel — the data-parallel path of bench.py (captured) and train.py (eager) —
+  on the PRODUCT ResNetSQ (its host-CPU path): the real backward drives the bucket all-reduces
+  through the post-accumulate-grad hooks, the buckets launch in reverse layer order (heads first,
+  stem last), and the averaged flat-buffer gradients equal the average of the per-rank
+  independent gradients; then train.py itself runs a 2-rank epoch (--device cpu) on that path.
+  (The CUDA side stream / event fork-join needs a GPU: tests/test_dp_graph_gpu.py.)
 """
 import os
 import socket
 import sys
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -85,7 +92,7 @@ def _worker(rank, world, port, tmpdir, q):
             fresh.load_state_dict(ck["model_state_dict"])
             res["epoch"] = ck["epoch"]
         # GraphDataParallel plumbing (the N-GPU graph path of bench.py): broadcast from rank 0, the
-        # flat gradient buffer, one SUM all-reduce, averaging scale handed to the optimizer
+        # flat gradient buffer, bucketed all-reduce, average
         from sqr import gradbuf
 
         class _Opt:
@@ -94,7 +101,7 @@ def _worker(rank, world, port, tmpdir, q):
         m2 = ref_torch.ResNetSQRef()
         opt2 = _Opt()
         gdp = sd.GraphDataParallel(m2, opt2, dev)
-        res["bcast_sum"] = float(sum(p.double().sum() for p in m2.parameters()))
+        res["bcast_sum"] = float(sum(p.detach().double().sum() for p in m2.parameters()))
         res["scale"] = opt2.sqr_grad_scale
         for i, p in enumerate(gdp.params):
             gradbuf.out(id(p), tuple(p.shape), dev).fill_(float(rank + 1) * (i + 1))
@@ -102,9 +109,51 @@ def _worker(rank, world, port, tmpdir, q):
         res["nbuckets"] = len(gdp.buckets)
         gdp.allreduce()
         res["flat_ok"] = all(
-            torch.all(gradbuf.out(id(p), tuple(p.shape), dev) == 3.0 * (i + 1)).item()
+            torch.all(gradbuf.out(id(p), tuple(p.shape), dev) == 1.5 * (i + 1)).item()
             for i, p in enumerate(gdp.params))
         gdp.close(opt2)
+
+        # GraphDataParallel driven by a real backward of the product model (host path)
+        import models
+        torch.manual_seed(7 + rank)  # different init per rank: the broadcast must equalise it
+        net3 = models.ResNetSQ(outputs=4, pretrained=False)
+        opt3 = torch.optim.SGD(net3.parameters(), lr=0.0)  # no sqr_grad_scale: the buffer is scaled
+        gdp3 = sd.GraphDataParallel(net3, opt3, dev, bucket_mb=8)
+        ref3 = models.ResNetSQ(outputs=4, pretrained=False)
+        ref3.load_state_dict(net3.state_dict())
+        opt3.zero_grad(set_to_none=True)
+        loss_of(net3, batches[rank]).backward()
+        res["launch_log_during_backward"] = list(gdp3.launch_log)
+        gdp3.allreduce()
+        gdp3.check_grads()
+        avg = None
+        for x in batches:
+            ref3.zero_grad(set_to_none=True)
+            loss_of(ref3, x).backward()
+            gr = [p.grad.clone() for p in ref3.parameters()]
+            avg = gr if avg is None else [a + b for a, b in zip(avg, gr)]
+        avg = [a / world for a in avg]
+        res["gdp_grad_rel_err"] = max(((p.grad - a).abs().max() / a.abs().max().clamp_min(1e-30)).item()
+                                      for p, a in zip(net3.parameters(), avg))
+        res["gdp_nbuckets"] = len(gdp3.buckets)
+        names = {id(p): n for n, p in net3.named_parameters()}
+        res["bucket_first_names"] = [names[mem[0]] for _, _, mem in gdp3.buckets]
+        # a second backward without clearing the gradients is refused
+        try:
+            loss_of(net3, batches[rank]).backward()
+            res["uncleared_refused"] = False
+        except RuntimeError:
+            res["uncleared_refused"] = True
+        gdp3.close(opt3)
+
+        # train.py on the same path: one 2-rank epoch on the host (config 1 plumbing, explicit loss)
+        import train
+        ck = os.path.join(tmpdir, "train_ck.pt")
+        tl, vl = train.main(["--device", "cpu", "--loss", "explicit", "--synthetic", "16", "--batch-size", "4",
+                             "--epochs", "1", "--render-size", "16", "--pretrained", "0",
+                             "--model-location", ck, "--log-interval", "100"])
+        res["train_loss"] = tl[0]
+        res["train_ck"] = os.path.exists(ck)
         sd.barrier()
         sd.finish()
         q.put((rank, res))
@@ -148,6 +197,18 @@ def test_ddp_gloo_world2(tmp_path):
         assert out[r]["grad_rel_err"] < 1e-5, out[r]["grad_rel_err"]
     assert out[0]["keys_prefixed"] is False and out[0]["epoch"] == 3
     assert out[0]["bcast_sum"] == out[1]["bcast_sum"]
-    assert out[0]["scale"] == out[1]["scale"] == 0.5
+    # host path: the buffer itself is averaged (the fused CUDA Adam would read it with scale 1/world)
+    assert out[0]["scale"] == out[1]["scale"] == 1.0
     assert out[0]["flat_ok"] and out[1]["flat_ok"]
     assert out[0]["nbuckets"] >= 2
+    for r in range(world):
+        assert out[r]["gdp_grad_rel_err"] < 1e-5, out[r]["gdp_grad_rel_err"]
+        nb = out[r]["gdp_nbuckets"]
+        assert nb >= 3
+        # every bucket but the stem's was all-reduced during the backward, in reverse layer order
+        assert out[r]["launch_log_during_backward"] == list(range(len(out[r]["launch_log_during_backward"])))
+        assert len(out[r]["launch_log_during_backward"]) >= nb - 1
+        assert out[r]["bucket_first_names"][0].startswith("output_rotation")
+        assert out[r]["uncleared_refused"]
+        assert np.isfinite(out[r]["train_loss"])
+    assert out[0]["train_ck"]

@@ -116,11 +116,11 @@ def test_implicit_grad_scales_with_upstream():
     np.testing.assert_allclose(p.grad.cpu().numpy(), 3 * g1, rtol=1e-6)
 
 
-def test_implicit_rejects_cpu_tensors_and_bad_shapes():
+def test_implicit_rejects_mixed_devices_and_bad_shapes():
     C = _classes()
     crit = C.ImplicitLoss(32, DEV)
     with pytest.raises(ValueError):
-        crit(torch.zeros(2, 1, 64, 64), torch.zeros(2, 12))
+        crit(torch.zeros(2, 1, 64, 64), torch.zeros(2, 12, device=DEV))
     with pytest.raises(ValueError):
         crit(torch.zeros(2, 1, 64, 64, device=DEV), torch.zeros(2, 11, device=DEV))
 
