@@ -62,6 +62,7 @@ struct NTMulti {
   NTArgs c[4];
   int start[4];
   int ncls;
+  unsigned long long* tp;  // nullable: clock probe slots
 };
 
 struct TNArgs {
@@ -72,6 +73,7 @@ struct TNArgs {
   float* slab;       // [splits][Kout][Ng]
   int ntm, ntn;
   int rect_wt;       // > 0: every BK-pixel tile is a rect_wt-wide rectangle of one image (no divides)
+  unsigned long long* tp;  // nullable: clock probe slots
 };
 
 // ============================================================================ NT (fwd / dgrad)
@@ -105,6 +107,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
   // LDS-DMA makes hipcc insert s_waitcnt vmcnt(0) in front of it (that killed the pipeline when
   // the tap table lived in LDS) — tap -> (r, s) is computed with a multiply-high instead.
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+  clock_begin(mc.tp);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -334,6 +337,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
       }
     }
   }
+  clock_end(mc.tp);
 }
 
 // ============================================================================ TN (wgrad)
@@ -358,6 +362,7 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   static_assert(QI >= 1 && PI >= 1, "tile too small for 4 waves");
   constexpr int TILE_Q = BK * QROWB, TILE_P = BK * PROWB, STAGE = TILE_Q + TILE_P;
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+  clock_begin(a.tp);
 
   const Gather& g = a.g;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -550,6 +555,7 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
       if (m < a.Kout) *(f32x4*)(slab + (size_t)m * a.Ng + n) = acc[j][i];
     }
   }
+  clock_end(a.tp);
 }
 
 // dw_kcrs[k][c][r][s] = sum_z slab[z][k][(r*S+s)*Ci + c]   (c < C real channels)
@@ -928,6 +934,7 @@ int launch_nt(NTArgs* cl, int ncls, hipStream_t st) {
   }
   for (int i = ncls; i < 4; ++i) mc.start[i] = total;
   mc.ncls = ncls;
+  mc.tp = probe_clock_take();
   const dim3 grid(total), blk(kNtThreads[cfg]);
   probe_begin(st);
   switch (cfg) {
@@ -972,6 +979,7 @@ int launch_tn(TNArgs a, const TNPlan& p, hipStream_t st) {
   a.ntm = p.ntm;
   a.ntn = p.ntn;
   a.kchunk = p.kchunk;
+  a.tp = probe_clock_take();
   const dim3 grid(p.ntm * p.ntn * p.splits), blk(256);
   probe_begin(st);
   if (p.bm == 128 && p.bn == 128) hipLaunchKernelGGL((conv_tn_kernel<T, 128, 128, 2, 2, 2>), grid, blk, 0, st, a);

@@ -26,7 +26,8 @@
 #define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop;
                    // conv3_kernel: 4 no per-tap wait/barrier, 8 no MFMA, 16 no fragment reads;
                    // conv3p_kernel: 128 no tap loop, 256 no output stores, 512 no row loads in
-                   // the tile loop, 1024 no fragment reads; conv3s2_dgrad_kernel: 2048 no dX
+                   // the tile loop, 1024 no fragment reads, 16384 no weight prologue, 32768 no
+                   // BatchNorm partials; conv3s2_dgrad_kernel: 2048 no dX
                    // stores, 4096 no MFMA, 8192 no weight loads after the prologue)
 #endif
 
@@ -372,7 +373,9 @@ __device__ __forceinline__ void wait_vm(int n) {
   }
 }
 
-template <typename T>
+// STATS: the forward's BatchNorm partials (a.stats != NULL); the backward-data launches skip the
+// per-tile accumulation entirely (it cost ~0.15 us per tile)
+template <typename T, bool STATS>
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
   // 2 x 2 waves, each 64 pixels (one image row) x 32 channels = two 32x32 MFMA accumulators
@@ -414,7 +417,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       const int tap = r / BN, n = r - tap * BN;
       wv[i] = (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4));
     }
+#if !(SQR_EXP & 16384)
     dma_pieces<WPW, NW>(wsrd, wl, wv, 0, wave);
+#endif
   }
   // LDS-DMA of input rows r0 .. r0+nrows-1 (row -1 / H: zero padding) into their ring slots; piece
   // p (8 LDS rows of one image row) goes to wave p % 4.  Returns this wave's instruction count.
@@ -532,14 +537,16 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       for (int g = 0; g < 4; ++g) {
         pk[i][g][0] = pack2<T>(acc[i][4 * g], acc[i][4 * g + 1]);
         pk[i][g][1] = pack2<T>(acc[i][4 * g + 2], acc[i][4 * g + 3]);
+#if !(SQR_EXP & 32768)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < 2 * STATS; ++q) {
           const float v0 = lo2f<T>(pk[i][g][q]), v1 = hi2f<T>(pk[i][g][q]);
           st1[4 * g + 2 * q] += v0;
           st2[4 * g + 2 * q] = fmaf(v0, v0, st2[4 * g + 2 * q]);
           st1[4 * g + 2 * q + 1] += v1;
           st2[4 * g + 2 * q + 1] = fmaf(v1, v1, st2[4 * g + 2 * q + 1]);
         }
+#endif
       }
     // tile k+1's rows (issued one iteration ago) have landed; younger in this wave's queue: the
     // stores of tile k-2, the row loads of tile k+2 and the stores of tile k-1
@@ -558,7 +565,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     __builtin_amdgcn_s_barrier();  // staged tile visible
   }
   if (ntile > 0) store_staged(ntile - 1);
-  if (a.stats) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
+  if (STATS && !(SQR_EXP & 32768)) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
     __syncthreads();
     float* red = (float*)ring;
     float* r1 = red + (wm * 32 + r32) * BN + wn * WN + 4 * h;
@@ -1178,7 +1185,12 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     const int grid = N * bpi;
     if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
     probe_begin(st);
-    SQR_DISPATCH16(dtype, T, hipLaunchKernelGGL(conv3p_kernel<T>, dim3(grid), dim3(256), 0, st, p));
+    SQR_DISPATCH16(dtype, T, {
+      if (stats)
+        hipLaunchKernelGGL((conv3p_kernel<T, true>), dim3(grid), dim3(256), 0, st, p);
+      else
+        hipLaunchKernelGGL((conv3p_kernel<T, false>), dim3(grid), dim3(256), 0, st, p);
+    });
     probe_end(st);
     SQR_HIP_LAUNCH_CHECK("conv3p_kernel");
     return 0;

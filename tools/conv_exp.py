@@ -1,0 +1,87 @@
+"""Time one conv kernel in isolation on the GPU: REPS launches captured in a HIP graph, each launch's
+own wall-clock span read back through the clock probe (sqr_probe_arm_clock), median over a few
+replays.  Used for kernel experiments (SQR_EXP ablation builds via SQR_LIB, tile configurations via
+SQR_D3_CFG / SQR_NT_CFG).
+
+    python tools/conv_exp.py --shape 64,64,64,64 --phase fwd [--dtype bf16] [--reps 20]
+Prints one JSON line: {"shape", "phase", "us": median per-launch us, "tflops", "lib"}.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sq-recovery_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="64,64,64,64", help="N,C,H,K (3x3 conv, square images)")
+    ap.add_argument("--stride", type=int, default=1)
+    ap.add_argument("--phase", default="fwd", choices=("fwd", "dgrad", "wgrad"))
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--replays", type=int, default=5)
+    a = ap.parse_args()
+    from sqr import conv as sc
+    from sqr._lib import LIB_PATH, check, lib
+    N, C, H, K = (int(v) for v in a.shape.split(","))
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float16
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    Ho = (H + 2 - 3) // a.stride + 1
+    x = torch.randn(N, C, H, H, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(N, K, Ho, Ho, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(K, C, 3, 3, device=dev, generator=g) / (9 * C) ** 0.5
+    d = sc._desc(N, C, H, H, K, 3, 3, a.stride, 1, dt)
+    krsc, crsk = sc.pack_weight(w, d, True)
+    clk = torch.empty(a.reps, 2, dtype=torch.int64, device=dev)
+
+    def one():
+        if a.phase == "fwd":
+            sc.conv2d_fwd(x, krsc, d, stats=True)
+        elif a.phase == "dgrad":
+            sc.conv2d_bwd_data(gy, crsk, d)
+        else:
+            sc.conv2d_bwd_weight(x, gy, d)
+
+    one()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        one()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    sc.set_probe(a.phase, N, C, H, K, 3, a.stride, clock=clk)
+    with torch.cuda.graph(graph):
+        for _ in range(a.reps):
+            one()
+    rows = sc.probe_clock_rows()
+    sc.set_probe(None, 0, 0, 0, 0, 0, 0)
+    khz = ctypes.c_int()
+    check(lib().sqr_wall_clock_khz(ctypes.byref(khz)), "khz")
+    spans = []
+    for _ in range(a.replays):
+        clk[:, 0].fill_(-1)
+        clk[:, 1].zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        v = clk[:rows].cpu()
+        ok = (v[:, 0] != -1) & (v[:, 1] > 0)
+        spans += [float(t) / khz.value * 1e3 for t in (v[ok, 1] - v[ok, 0]).tolist()]
+    us = float(np.median(spans)) if spans else float("nan")
+    flops = 2.0 * N * Ho * Ho * K * C * 9
+    print(json.dumps({"shape": a.shape, "stride": a.stride, "phase": a.phase, "dtype": a.dtype, "us": us,
+                      "tflops": flops / us / 1e6 if spans else None, "n": len(spans),
+                      "lib": os.path.basename(LIB_PATH), "env": {k: v for k, v in os.environ.items()
+                                                                 if k.startswith("SQR_")}}))
+
+
+if __name__ == "__main__":
+    main()
