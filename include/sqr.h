@@ -214,25 +214,25 @@ int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t* argmax, co
                  int C, int dtype, const float* gamma, const float* save_mean, const float* save_invstd, void* dx,
                  float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 
-/* ---------------------------------------------------------------- fused stem (bf16) */
+/* ---------------------------------------------------------------- fused stem (bf16 / fp16) */
 
-/* resnet18 stem of ResNetSQ (torch/models.py:181-184) for bf16 training / inference:
+/* resnet18 stem of ResNetSQ (torch/models.py:181-184) for 16-bit training / inference:
  * y = maxpool3x3/s2/p1(relu(bn1(conv1(x)))), conv1 = 1 -> 64 channels, 7x7, stride 2, pad 3, no
- * bias, computed in bf16 (fp32 accumulation) WITHOUT materialising the conv1 activation: the
- * forward recomputes conv1 for the BatchNorm statistics and for the pooling, the backward
- * recomputes it and forms dW / dgamma / dbeta in closed form (no input gradient).
- *   x [N][H][W] (x_dtype f32 or bf16), w [64][1][7][7] f32, y [N][Hp][Wp][64] bf16 (NHWC),
+ * bias, computed in y_dtype (bf16 or fp16; fp32 accumulation) WITHOUT materialising the conv1
+ * activation: the forward recomputes conv1 for the BatchNorm statistics and for the pooling, the
+ * backward recomputes it and forms dW / dgamma / dbeta in closed form (no input gradient).
+ *   x [N][H][W] (x_dtype f32, bf16 or fp16), w [64][1][7][7] f32, y [N][Hp][Wp][64] y_dtype (NHWC),
  *   argmax [N][Hp][Wp][64] u8 (window tap of the first maximum; written when training).
  * Shapes: the conv1 output (H/2 x W/2) must tile by 8 x 32 and the pooled one by 8 x 16
  * (sqr_stem_fused_supported).  BatchNorm semantics as sqr_stem_fwd (momentum, running stats). */
 int sqr_stem_fused_supported(int N, int H, int W);
 size_t sqr_stem_fused_workspace_bytes(int N, int H, int W);
-int sqr_stem_fused_fwd(const void* x, int x_dtype, int N, int H, int W, const float* w, const float* gamma,
+int sqr_stem_fused_fwd(const void* x, int x_dtype, int y_dtype, int N, int H, int W, const float* w, const float* gamma,
                        const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                        int training, void* y, uint8_t* argmax, float* save_mean, float* save_invstd,
                        void* workspace, size_t workspace_bytes, void* stream);
 /* dy, y, argmax: the pooled gradient / output / argmax of the forward; dw [64][1][7][7] f32 */
-int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int W, const float* w, const float* gamma,
+int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N, int H, int W, const float* w, const float* gamma,
                        const float* save_mean, const float* save_invstd, const void* dy, const void* y,
                        const uint8_t* argmax, float* dw, float* dgamma, float* dbeta, void* workspace,
                        size_t workspace_bytes, void* stream);

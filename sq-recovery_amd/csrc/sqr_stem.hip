@@ -1,4 +1,4 @@
-// Fused ResNet stem for bf16 training / inference: conv1 (1 -> 64 channels, 7x7, stride 2, pad 3,
+// Fused ResNet stem for bf16 / fp16 training / inference: conv1 (1 -> 64 channels, 7x7, stride 2, pad 3,
 // no bias) + bn1 + ReLU + max-pool(3, 2, 1) of ResNetSQ's resnet18 encoder (torch/models.py:181-184:
 // the grayscale conv1 is the ImageNet kernel summed over RGB), WITHOUT materialising the conv1
 // activation in HBM.
@@ -24,7 +24,9 @@
 //            is linear in (g, x, 1), so  dW = a*T1 + k3*T2 + k2*T3  and dgamma / dbeta follow from
 //            the two sums: dx itself is never formed.
 //
-// conv1 as MFMA (v_mfma_f32_16x16x32_bf16): rows = 64 output channels (4 blocks of 16), columns =
+// Activations T = bf16 or fp16 (the network's autocast dtype; every "bf16" below reads "T").
+//
+// conv1 as MFMA (v_mfma_f32_16x16x32_{bf16,f16}): rows = 64 output channels (4 blocks of 16), columns =
 // 16 pixels, k = 64 taps (r, s) = (j / 8, j % 8), r, s < 7 real, the padding taps carry zero
 // weight.  A lane's 8 consecutive taps are one input row segment x[2h-3+r][2w-3 .. 2w+4]: 4
 // aligned ds_read_b32 from the LDS window (column offset 4*(w-w0) bytes).  Weights live in
@@ -38,6 +40,8 @@ namespace stemf {
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -47,26 +51,50 @@ constexpr int WPITCH = 72;       // LDS window row pitch (elements): 144 B, a mu
 constexpr int GRID_PERSIST = 512;  // persistent grids (fixed: the partial-sum order is part of the result)
 constexpr int PART_BWD = 2 * KC * KC + 3 * KC;  // T1, T2, T3, sum g, sum g*x
 
+template <typename T> struct TT;
+template <> struct TT<bf16> {
+  typedef bf16x8 V8;
+  static constexpr uint32_t NEG_INF2 = 0xff80ff80u;  // a packed pair of -inf
+};
+template <> struct TT<f16> {
+  typedef f16x8 V8;
+  static constexpr uint32_t NEG_INF2 = 0xfc00fc00u;
+};
+template <typename T> using V8 = typename TT<T>::V8;
+
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ float bf(float v) { return (float)(bf16)v; }  // round to bf16 (RNE)
-__device__ __forceinline__ uint16_t bfbits(float v) { return __builtin_bit_cast(uint16_t, (bf16)v); }
-__device__ __forceinline__ float bits2f(uint32_t b16) { return __uint_as_float(b16 << 16); }
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-// two floats -> packed bf16 pair (RNE; v_cvt_pk_bf16_f32), lo in bits 0..15
-__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+__device__ __forceinline__ f32x4 mfma(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
-// ReLU of a packed bf16 pair as signed 16-bit max with 0 (negative values and -0 -> +0)
+template <typename T> __device__ __forceinline__ float rnd(float v) { return (float)(T)v; }  // round to T (RNE)
+template <typename T> __device__ __forceinline__ uint16_t hbits(float v) { return __builtin_bit_cast(uint16_t, (T)v); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+// two floats -> packed 16-bit pair (RNE), lo in bits 0..15
+template <typename T> __device__ __forceinline__ uint32_t pk16(float lo, float hi) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, t2));
+}
+// the halves of a packed pair as floats
+template <typename T> __device__ __forceinline__ float plo(uint32_t p) {
+  if constexpr (__is_same(T, bf16)) return __uint_as_float(p << 16);
+  else return (float)__builtin_bit_cast(f16, (uint16_t)(p & 0xffffu));
+}
+template <typename T> __device__ __forceinline__ float phi(uint32_t p) {
+  if constexpr (__is_same(T, bf16)) return __uint_as_float(p & 0xffff0000u);
+  else return (float)__builtin_bit_cast(f16, (uint16_t)(p >> 16));
+}
+// ReLU of a packed pair as signed 16-bit max with 0 (negative values and -0 -> +0; bf16 and fp16
+// keep the sign in bit 15 and order non-negative values like integers)
 __device__ __forceinline__ uint32_t pk_relu(uint32_t v) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), s16x2{0, 0}));
 }
 
-// weight fragments: wf[jb][ks][i] = bf16(w[16 jb + fr][r = 4 ks + fq][s = i]) (0 for r or s == 7)
-__device__ __forceinline__ void load_wfrag(const float* __restrict__ w, int lane, bf16x8 (&wf)[4][2]) {
+// weight fragments: wf[jb][ks][i] = T(w[16 jb + fr][r = 4 ks + fq][s = i]) (0 for r or s == 7)
+template <typename T>
+__device__ __forceinline__ void load_wfrag(const float* __restrict__ w, int lane, V8<T> (&wf)[4][2]) {
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
@@ -75,13 +103,14 @@ __device__ __forceinline__ void load_wfrag(const float* __restrict__ w, int lane
       const int r = 4 * ks + fq;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        wf[jb][ks][i] = (bf16)((r < 7 && i < 7) ? w[(16 * jb + fr) * 49 + r * 7 + i] : 0.f);
+        wf[jb][ks][i] = (T)((r < 7 && i < 7) ? w[(16 * jb + fr) * 49 + r * 7 + i] : 0.f);
     }
 }
 
 // conv1 of 16 pixels: lane (fr, fq) supplies pixel fr, whose tap (0, 0) sits at byte woff of the
 // window; acc[jb][e] = x[pixel fr][channel 16 jb + 4 fq + e] (fp32)
-__device__ __forceinline__ void conv_block(const char* win, int woff, int lane, const bf16x8 (&wf)[4][2],
+template <typename T>
+__device__ __forceinline__ void conv_block(const char* win, int woff, int lane, const V8<T> (&wf)[4][2],
                                            f32x4 (&acc)[4]) {
   const int fq = lane >> 4;
 #pragma unroll
@@ -91,7 +120,7 @@ __device__ __forceinline__ void conv_block(const char* win, int woff, int lane, 
     const char* p = win + woff + (4 * ks + fq) * (WPITCH * 2);
     const u32x4 u = {*(const uint32_t*)p, *(const uint32_t*)(p + 4), *(const uint32_t*)(p + 8),
                      *(const uint32_t*)(p + 12)};
-    const bf16x8 a = __builtin_bit_cast(bf16x8, u);
+    const V8<T> a = __builtin_bit_cast(V8<T>, u);
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) acc[jb] = mfma(wf[jb][ks], a, acc[jb]);
   }
@@ -100,7 +129,7 @@ __device__ __forceinline__ void conv_block(const char* win, int woff, int lane, 
 // Input window rows [y0, y0 + WR) x cols [x0, x0 + WC) staged through registers: load() issues
 // the (branch-free, clamped) global loads of a tile early, store() writes them as bf16 into the LDS
 // window (pitch WPITCH) — the persistent loops prefetch tile t+1 while tile t computes.
-template <typename TI, int WR, int WC>
+template <typename TI, typename T, int WR, int WC>
 struct Window {
   static constexpr int NE = WR * WC, KW = (NE + 255) / 256;
   float v[KW];
@@ -121,14 +150,14 @@ struct Window {
     for (int k = 0; k < KW; ++k) {
       const int i = threadIdx.x + 256 * k;
       const int r = i / WC, c = i - r * WC;
-      if (i < NE) win[r * WPITCH + c] = bfbits(v[k]);
+      if (i < NE) win[r * WPITCH + c] = hbits<T>(v[k]);
     }
   }
 };
 
 // ---------------------------------------------------------------- S1: BN statistics
 // tile = 8 conv rows x 32 conv cols (16 MFMA pixel blocks, 4 per wave); window 22 x 70
-template <typename TI>
+template <typename TI, typename T>
 __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ img, const float* __restrict__ w,
                                                          int H, int W, int tiles_x, int tiles_img, int ntiles,
                                                          float* __restrict__ part) {
@@ -136,12 +165,12 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
   uint16_t* win = (uint16_t*)smem;
   float* red = (float*)(smem + 22 * WPITCH * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  bf16x8 wf[4][2];
-  load_wfrag(w, lane, wf);
+  V8<T> wf[4][2];
+  load_wfrag<T>(w, lane, wf);
   float s1[16], s2[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) s1[i] = s2[i] = 0.f;
-  Window<TI, 22, 70> pf;
+  Window<TI, T, 22, 70> pf;
   auto fetch = [&](int t) {
     const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
     pf.load(img + (size_t)n * H * W, H, W, 16 * ty - 3, 64 * tx - 3);
@@ -156,13 +185,13 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
     for (int b = 0; b < 4; ++b) {
       const int q = (wave * 4 + b) * 16 + fr, py = q >> 5, px = q & 31;
       f32x4 acc[4];
-      conv_block((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
+      conv_block<T>((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
       // every tile pixel is a real conv output (Hc % 8 == 0, Wc % 32 == 0 checked on the host)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float v = bf(acc[jb][e]);
+          const float v = rnd<T>(acc[jb][e]);
           s1[jb * 4 + e] += v;
           s2[jb * 4 + e] = fmaf(v, v, s2[jb * 4 + e]);
         }
@@ -209,17 +238,17 @@ constexpr int TPITCH = KC * 2 + 16;  // conv tile pixel pitch (bytes): 144 = 36 
 constexpr int S2_LDS = S2_WIN + PPIX * TPITCH;
 static_assert(S2_WC <= WPITCH, "window pitch");
 
-template <typename TI>
+template <typename TI, typename T>
 __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ img, const float* __restrict__ w,
                                                         const float* __restrict__ coef, int H, int W, int Hc, int Wc,
                                                         int Hp, int Wp, int ptx, int ptiles_img, int ntiles,
-                                                        bf16* __restrict__ y, uint8_t* __restrict__ argmax) {
+                                                        T* __restrict__ y, uint8_t* __restrict__ argmax) {
   __shared__ __attribute__((aligned(16))) char smem[S2_LDS];
   uint16_t* win = (uint16_t*)smem;
   char* tile = smem + S2_WIN;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  bf16x8 wf[4][2];
-  load_wfrag(w, lane, wf);
+  V8<T> wf[4][2];
+  load_wfrag<T>(w, lane, wf);
   float sc[16], sh[16];
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
@@ -228,7 +257,7 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
       sc[jb * 4 + e] = coef[16 * jb + 4 * fq + e];
       sh[jb * 4 + e] = coef[KC + 16 * jb + 4 * fq + e];
     }
-  Window<TI, S2_WR, S2_WC> pf;
+  Window<TI, T, S2_WR, S2_WC> pf;
   auto fetch = [&](int t) {
     const int n = t / ptiles_img, rem = t - n * ptiles_img, pty = rem / ptx, ptxx = rem - pty * ptx;
     pf.load(img + (size_t)n * H * W, H, W, 2 * (2 * pty * PTH - 1) - 3, 2 * (2 * ptxx * PTW - 1) - 3);
@@ -247,7 +276,7 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
       const int qc = q < PPIX ? q : PPIX - 1;
       const int row = qc / PC, col = qc - row * PC;
       f32x4 acc[4];
-      conv_block((const char*)win, 2 * row * WPITCH * 2 + 4 * col, lane, wf, acc);
+      conv_block<T>((const char*)win, 2 * row * WPITCH * 2 + 4 * col, lane, wf, acc);
       const int hc = ch0 + row, wc = cw0 + col;
       const bool inside = (unsigned)hc < (unsigned)Hc && (unsigned)wc < (unsigned)Wc;
       if (q < PPIX) {
@@ -256,12 +285,12 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
           uint32_t pk[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            // the unfused path: bf16 conv output -> relu(x * scale + shift) -> rounded to bf16
+            // the unfused path: T conv output -> relu(x * scale + shift) -> rounded to T
             const int i0 = jb * 4 + 2 * h, i1 = i0 + 1;
-            const uint32_t xb = pk_bf16(acc[jb][2 * h], acc[jb][2 * h + 1]);
-            const float t0 = fmaf(__uint_as_float(xb << 16), sc[i0], sh[i0]);
-            const float t1 = fmaf(__uint_as_float(xb & 0xffff0000u), sc[i1], sh[i1]);
-            pk[h] = inside ? pk_relu(pk_bf16(t0, t1)) : 0xff80ff80u;  // bf16 -inf outside the image
+            const uint32_t xb = pk16<T>(acc[jb][2 * h], acc[jb][2 * h + 1]);
+            const float t0 = fmaf(plo<T>(xb), sc[i0], sh[i0]);
+            const float t1 = fmaf(phi<T>(xb), sc[i1], sh[i1]);
+            pk[h] = inside ? pk_relu(pk16<T>(t0, t1)) : TT<T>::NEG_INF2;  // -inf outside the image
           }
           *(u32x2*)(tile + (size_t)q * TPITCH + (16 * jb + 4 * fq) * 2) = u32x2{pk[0], pk[1]};
         }
@@ -274,7 +303,7 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
       const int it = tid + 256 * k;
       const int cg = it & 7, pp = it >> 3, i = pp / PTW, j = pp - i * PTW;
       // max over the window of the key (value bits << 16 | 15 - tap) as signed int: the values are
-      // bf16 relu outputs (>= +0, integer-ordered) or -inf (negative); on equal values the larger
+      // 16-bit relu outputs (>= +0, integer-ordered) or -inf (negative); on equal values the larger
       // key is the smaller tap, i.e. torch's first maximum in row-major window order
       int best[8];
 #pragma unroll
@@ -331,7 +360,8 @@ struct PoolIn {
   uint32_t valid;  // bit a*2+b: window inside the pooled grid
 };
 
-__device__ __forceinline__ void pool_load(PoolIn& pi, const bf16* __restrict__ dpool, const bf16* __restrict__ ypool,
+template <typename T>
+__device__ __forceinline__ void pool_load(PoolIn& pi, const T* __restrict__ dpool, const T* __restrict__ ypool,
                                           const uint8_t* __restrict__ argmax, int n, int K, int J, int Hp, int Wp,
                                           int cg) {
   pi.valid = 0;
@@ -348,10 +378,10 @@ __device__ __forceinline__ void pool_load(PoolIn& pi, const bf16* __restrict__ d
     }
 }
 
-template <typename TI>
+template <typename TI, typename T>
 __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__ img, const float* __restrict__ w,
-                                                          const bf16* __restrict__ dpool,
-                                                          const bf16* __restrict__ ypool,
+                                                          const T* __restrict__ dpool,
+                                                          const T* __restrict__ ypool,
                                                           const uint8_t* __restrict__ argmax, int H, int W, int Hp,
                                                           int Wp, int tiles_x, int tiles_img, int ntiles,
                                                           float* __restrict__ part) {
@@ -360,11 +390,11 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
   char* AT = smem + 2048;
   char* GT = AT + S3_IMG;
   char* XT = GT + S3_IMG;
-  bf16x8* WF = (bf16x8*)(XT + S3_IMG);
+  V8<T>* WF = (V8<T>*)(XT + S3_IMG);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   if (wave == 0) {
-    bf16x8 wf[4][2];
-    load_wfrag(w, lane, wf);
+    V8<T> wf[4][2];
+    load_wfrag<T>(w, lane, wf);
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
@@ -373,9 +403,9 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
   f32x4 T1[4], T2[4], T3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb) T1[jb] = T2[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 ones;
+  V8<T> ones;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.f;
+  for (int i = 0; i < 8; ++i) ones[i] = (T)1.f;
   // g items: thread = (quad = tid >> 3 of 2 x 16 quads, channel group cg = tid & 7)
   const int cg = tid & 7, quad = tid >> 3, qy = quad >> 4, qx = quad & 15;
   float sg[8], sgx[8];
@@ -384,7 +414,7 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
   const int oct = tid & 15;  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
 
   // register prefetch of the next tile's input window and pooled-gradient inputs
-  Window<TI, 14, 70> pw;
+  Window<TI, T, 14, 70> pw;
   PoolIn pin;
   auto fetch = [&](int t) {
     const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
@@ -397,7 +427,7 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
     pw.store(win);
     // the pooled inputs of this tile, reduced to what the routing needs: per window and channel the
     // argmax tap and the gradient masked by (window valid, pooled output > 0)
-    uint32_t amw[4][2], dvp[4][4];  // dvp: bf16 pairs of the masked gradient
+    uint32_t amw[4][2], dvp[4][4];  // dvp: 16-bit pairs of the masked gradient
 #pragma unroll
     for (int wd = 0; wd < 4; ++wd) {
       const bool ok = (pin.valid >> wd) & 1u;
@@ -405,7 +435,7 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
       amw[wd][1] = pin.am[wd][1];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
-        // pooled values are relu outputs (>= 0): y > 0 <=> its bf16 bits are non-zero
+        // pooled values are relu outputs (>= +0): y > 0 <=> its 16-bit pattern is non-zero
         const uint32_t y2 = pin.yp[wd][h], d2 = pin.dp[wd][h];
         const uint32_t mlo = (ok && (y2 & 0xffffu)) ? 0xffffu : 0u, mhi = (ok && (y2 >> 16)) ? 0xffff0000u : 0u;
         dvp[wd][h] = d2 & (mlo | mhi);
@@ -417,17 +447,17 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
 #pragma unroll 1
     for (int b = 0; b < 2; ++b) {
       const int p = (wave * 2 + b) * 16 + fr, py = p >> 5, px = p & 31;
-      bf16x8 wf[4][2];
+      V8<T> wf[4][2];
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) wf[jb][ks] = WF[(jb * 2 + ks) * 64 + lane];
       f32x4 acc[4];
-      conv_block((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
+      conv_block<T>((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) *(uint16_t*)(XT + img_off(16 * jb + 4 * fq + e, p)) = bfbits(acc[jb][e]);
+        for (int e = 0; e < 4; ++e) *(uint16_t*)(XT + img_off(16 * jb + 4 * fq + e, p)) = hbits<T>(acc[jb][e]);
     }
     // (b) A^T from the window
 #pragma unroll
@@ -459,7 +489,7 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
               if (dh < 0 || dw < 0) continue;
               const uint32_t ae = (amw[a * 2 + b][e >> 2] >> (8 * (e & 3))) & 0xffu;
               const uint32_t d2 = dvp[a * 2 + b][e >> 1];
-              const float dv = (e & 1) ? __uint_as_float(d2 & 0xffff0000u) : __uint_as_float(d2 << 16);
+              const float dv = (e & 1) ? phi<T>(d2) : plo<T>(d2);
               acc += ae == (uint32_t)(dh * 3 + dw) ? dv : 0.f;
             }
           g[px][e] = acc;
@@ -471,8 +501,8 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
         const uint32_t xx = *(const uint32_t*)(XT + img_off(c, p0));
         const float g0 = g[0][e], g1 = g[1][e];
         sg[e] += g0 + g1;
-        sgx[e] = fmaf(g0, __uint_as_float(xx << 16), fmaf(g1, __uint_as_float(xx & 0xffff0000u), sgx[e]));
-        *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)bfbits(g0) | ((uint32_t)bfbits(g1) << 16);
+        sgx[e] = fmaf(g0, plo<T>(xx), fmaf(g1, phi<T>(xx), sgx[e]));
+        *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)hbits<T>(g0) | ((uint32_t)hbits<T>(g1) << 16);
       }
     }
     __syncthreads();
@@ -482,16 +512,16 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
     for (int ks = 0; ks < 4; ++ks) {
       const int p = 32 * ks + 8 * fq;
       const int ch = 16 * wave + fr;
-      const bf16x8 gfr = *(const bf16x8*)(GT + img_off(ch, p));
-      const bf16x8 xfr = *(const bf16x8*)(XT + img_off(ch, p));
+      const V8<T> gfr = *(const V8<T>*)(GT + img_off(ch, p));
+      const V8<T> xfr = *(const V8<T>*)(XT + img_off(ch, p));
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
-        const bf16x8 afr = *(const bf16x8*)(AT + img_off(16 * jb + fr, p));
+        const V8<T> afr = *(const V8<T>*)(AT + img_off(16 * jb + fr, p));
         T1[jb] = mfma(gfr, afr, T1[jb]);
         T2[jb] = mfma(xfr, afr, T2[jb]);
       }
       // (MFMA ignores EXEC: no lane-divergent branch around it)
-      T3 = mfma(ones, *(const bf16x8*)(AT + img_off(ch, p)), T3);
+      T3 = mfma(ones, *(const V8<T>*)(AT + img_off(ch, p)), T3);
     }
   }
 
@@ -614,24 +644,41 @@ extern "C" size_t sqr_stem_fused_workspace_bytes(int N, int H, int W) {
   return fwd > bwd ? fwd : bwd;
 }
 
-template <typename TI>
+template <typename TI, typename T>
 static void launch_stats(const void* x, int N, int H, int W, const StemGeom& g, const float* w, float* part, int grid,
                          hipStream_t st) {
   const int tiles_x = g.Wc / 32, tiles_img = (g.Hc / 8) * tiles_x;
-  hipLaunchKernelGGL(stem_stats_kernel<TI>, dim3(grid), dim3(256), 0, st, (const TI*)x, w, H, W, tiles_x, tiles_img,
+  hipLaunchKernelGGL((stem_stats_kernel<TI, T>), dim3(grid), dim3(256), 0, st, (const TI*)x, w, H, W, tiles_x, tiles_img,
                      N * tiles_img, part);
 }
 
-template <typename TI>
+template <typename TI, typename T>
 static void launch_pool(const void* x, int N, int H, int W, const StemGeom& g, const float* w, const float* coef,
                         void* y, uint8_t* argmax, hipStream_t st) {
   const int ptx = g.Wp / PTW, ptiles_img = (g.Hp / PTH) * ptx, ntiles = N * ptiles_img;
   const int grid = ntiles < 768 ? ntiles : 768;  // persistent: 3 workgroups per CU
-  hipLaunchKernelGGL(stem_pool_kernel<TI>, dim3(grid), dim3(256), 0, st, (const TI*)x, w, coef, H, W, g.Hc, g.Wc,
-                     g.Hp, g.Wp, ptx, ptiles_img, ntiles, (bf16*)y, argmax);
+  hipLaunchKernelGGL((stem_pool_kernel<TI, T>), dim3(grid), dim3(256), 0, st, (const TI*)x, w, coef, H, W, g.Hc,
+                     g.Wc, g.Hp, g.Wp, ptx, ptiles_img, ntiles, (T*)y, argmax);
 }
 
-extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int N, int H, int W, const float* w, const float* gamma,
+// dispatch over (input dtype TI in f32 / bf16 / f16) x (activation dtype T in bf16 / f16)
+#define SQR_STEM_DISPATCH(x_dtype, y_dtype, CALL)                                          \
+  do {                                                                                     \
+    if ((y_dtype) == SQR_DTYPE_F16) {                                                      \
+      typedef f16 T;                                                                       \
+      if ((x_dtype) == SQR_DTYPE_BF16) { typedef bf16 TI; CALL; }                          \
+      else if ((x_dtype) == SQR_DTYPE_F16) { typedef f16 TI; CALL; }                       \
+      else { typedef float TI; CALL; }                                                     \
+    } else {                                                                               \
+      typedef bf16 T;                                                                      \
+      if ((x_dtype) == SQR_DTYPE_BF16) { typedef bf16 TI; CALL; }                          \
+      else if ((x_dtype) == SQR_DTYPE_F16) { typedef f16 TI; CALL; }                       \
+      else { typedef float TI; CALL; }                                                     \
+    }                                                                                      \
+  } while (0)
+
+extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int y_dtype, int N, int H, int W, const float* w,
+                                  const float* gamma,
                                   const float* beta, float* running_mean, float* running_var, float momentum, float eps,
                                   int training, void* y, uint8_t* argmax, float* save_mean, float* save_invstd,
                                   void* workspace, size_t workspace_bytes, void* stream) {
@@ -639,7 +686,9 @@ extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int N, int H, int 
   int rc = stem_geom(N, H, W, &g);
   if (rc) return rc;
   SQR_CHECK_ARG(x && w && y && workspace, "stem_fused_fwd: null pointer");
-  SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16, "stem_fused_fwd: bad x dtype");
+  SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16 || x_dtype == SQR_DTYPE_F16,
+                "stem_fused_fwd: bad x dtype");
+  SQR_CHECK_ARG(y_dtype == SQR_DTYPE_BF16 || y_dtype == SQR_DTYPE_F16, "stem_fused_fwd: bad y dtype");
   SQR_CHECK_ARG(!training || (save_mean && save_invstd), "stem_fused_fwd: training needs save_mean/save_invstd");
   SQR_CHECK_ARG(training || (running_mean && running_var), "stem_fused_fwd: eval needs running statistics");
   if (workspace_bytes < sqr_stem_fused_workspace_bytes(N, H, W)) {
@@ -652,8 +701,7 @@ extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int N, int H, int 
   if (training) {
     const int ntiles = N * (g.Hc / 8) * (g.Wc / 32);
     const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;
-    if (x_dtype == SQR_DTYPE_BF16) launch_stats<bf16>(x, N, H, W, g, w, part, grid, st);
-    else launch_stats<float>(x, N, H, W, g, w, part, grid, st);
+    SQR_STEM_DISPATCH(x_dtype, y_dtype, (launch_stats<TI, T>(x, N, H, W, g, w, part, grid, st)));
     SQR_HIP_LAUNCH_CHECK("stem_stats_kernel");
     rc = bn_finalize_partials(part, grid, (long long)N * g.Hc * g.Wc, KC, gamma, beta, running_mean, running_var,
                               momentum, eps, save_mean, save_invstd, coef, st);
@@ -661,13 +709,13 @@ extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int N, int H, int 
     rc = bn_infer_coef(KC, gamma, beta, running_mean, running_var, eps, coef, st);
   }
   if (rc) return rc;
-  if (x_dtype == SQR_DTYPE_BF16) launch_pool<bf16>(x, N, H, W, g, w, coef, y, training ? argmax : nullptr, st);
-  else launch_pool<float>(x, N, H, W, g, w, coef, y, training ? argmax : nullptr, st);
+  SQR_STEM_DISPATCH(x_dtype, y_dtype, (launch_pool<TI, T>(x, N, H, W, g, w, coef, y, training ? argmax : nullptr, st)));
   SQR_HIP_LAUNCH_CHECK("stem_pool_kernel");
   return 0;
 }
 
-extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int W, const float* w, const float* gamma,
+extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N, int H, int W, const float* w,
+                                  const float* gamma,
                                   const float* save_mean, const float* save_invstd, const void* dy, const void* y,
                                   const uint8_t* argmax, float* dw, float* dgamma, float* dbeta, void* workspace,
                                   size_t workspace_bytes, void* stream) {
@@ -676,7 +724,9 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int 
   if (rc) return rc;
   SQR_CHECK_ARG(x && w && save_mean && save_invstd && dy && y && argmax && dw && workspace,
                 "stem_fused_bwd: null pointer");
-  SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16, "stem_fused_bwd: bad x dtype");
+  SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16 || x_dtype == SQR_DTYPE_F16,
+                "stem_fused_bwd: bad x dtype");
+  SQR_CHECK_ARG(y_dtype == SQR_DTYPE_BF16 || y_dtype == SQR_DTYPE_F16, "stem_fused_bwd: bad y dtype");
   if (workspace_bytes < sqr_stem_fused_workspace_bytes(N, H, W)) {
     set_error("stem_fused_bwd: workspace too small");
     return SQR_E_WORKSPACE;
@@ -685,12 +735,10 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int N, int H, int 
   float* part = (float*)workspace;
   const int tiles_x = g.Wc / 32, tiles_img = (g.Hc / 4) * tiles_x, ntiles = N * tiles_img;
   const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;
-  if (x_dtype == SQR_DTYPE_BF16)
-    hipLaunchKernelGGL(stem_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, st, (const bf16*)x, w, (const bf16*)dy,
-                       (const bf16*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles, part);
-  else
-    hipLaunchKernelGGL(stem_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, w, (const bf16*)dy,
-                       (const bf16*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles, part);
+  SQR_STEM_DISPATCH(x_dtype, y_dtype,
+                    hipLaunchKernelGGL((stem_bwd_kernel<TI, T>), dim3(grid), dim3(256), 0, st, (const TI*)x, w,
+                                       (const T*)dy, (const T*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles,
+                                       part));
   SQR_HIP_LAUNCH_CHECK("stem_bwd_kernel");
   double* tot = (double*)((char*)workspace + a256((size_t)GRID_PERSIST * PART_BWD * 4));
   hipLaunchKernelGGL(colsum_kernel, dim3((PART_BWD + 63) / 64), dim3(256), 0, st, (const float*)part, grid, PART_BWD,

@@ -98,10 +98,10 @@ SIGNATURES = {
                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_stem_fused_supported": (c_int, [c_int, c_int, c_int]),
     "sqr_stem_fused_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
-    "sqr_stem_fused_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+    "sqr_stem_fused_fwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),
-    "sqr_stem_fused_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+    "sqr_stem_fused_bwd": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                    c_void_p]),
     "sqr_adam_step": (c_int, [ctypes.POINTER(SqrAdamParam), c_int, c_double, c_double, c_double, c_double,

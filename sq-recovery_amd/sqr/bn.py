@@ -199,21 +199,23 @@ def stem(x, bn, counted=False):
 
 
 class FusedStemFn(torch.autograd.Function):
-    """maxpool3x3/2/1(relu(bn1(conv1(x)))) for the 1-channel ResNetSQ input in ONE bf16 op
-    (libsqr sqr_stem_fused_*): the conv1 activation never reaches HBM; backward gives the conv1
-    weight and BN parameter gradients (the input image needs no gradient)."""
+    """maxpool3x3/2/1(relu(bn1(conv1(x)))) for the 1-channel ResNetSQ input in ONE 16-bit op
+    (libsqr sqr_stem_fused_*; activations bf16 or fp16 = `dt`): the conv1 activation never reaches
+    HBM; backward gives the conv1 weight and BN parameter gradients (the input image needs no
+    gradient)."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, rmean, rvar, training, momentum, eps):
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, training, momentum, eps, dt):
         N, _, H, W = x.shape
         x = x.contiguous()
-        xdt = 1 if x.dtype == torch.bfloat16 else 0
-        if x.dtype not in (torch.float32, torch.bfloat16):
+        if x.dtype not in (torch.float32, torch.bfloat16, torch.float16):
             x = x.float()
+        xdt = _dt(x)
+        ydt = _dt(torch.empty(0, dtype=dt))
         L = lib()
         Hc, Wc = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         Hp, Wp = (Hc - 1) // 2 + 1, (Wc - 1) // 2 + 1
-        y = torch.empty((N, 64, Hp, Wp), dtype=torch.bfloat16, device=x.device, memory_format=_CL)
+        y = torch.empty((N, 64, Hp, Wp), dtype=dt, device=x.device, memory_format=_CL)
         arg = torch.empty((N, Hp, Wp, 64), dtype=torch.uint8, device=x.device) if training else None
         f32 = dict(dtype=torch.float32, device=x.device)
         mean, invstd = torch.empty(64, **f32), torch.empty(64, **f32)
@@ -222,12 +224,12 @@ class FusedStemFn(torch.autograd.Function):
         wf = w.detach().float().contiguous()
         rm = ptr(rmean) if rmean is not None else ctypes.c_void_p(0)
         rv = ptr(rvar) if rvar is not None else ctypes.c_void_p(0)
-        check(L.sqr_stem_fused_fwd(ptr(x), xdt, N, H, W, ptr(wf), ptr(gamma), ptr(beta), rm, rv,
+        check(L.sqr_stem_fused_fwd(ptr(x), xdt, ydt, N, H, W, ptr(wf), ptr(gamma), ptr(beta), rm, rv,
                                    ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(y), ptr(arg),
                                    ptr(mean), ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_stem_fused_fwd")
         if not training:
             ctx.mark_non_differentiable(y)
-        ctx.xdt = xdt
+        ctx.xdt, ctx.ydt, ctx.dt = xdt, ydt, dt
         ctx.pids = (id(w), id(gamma), id(beta))
         ctx.save_for_backward(x, wf, gamma, y, arg, mean, invstd)
         return y
@@ -238,22 +240,22 @@ class FusedStemFn(torch.autograd.Function):
         if arg is None:
             raise RuntimeError("sqr fused stem: backward through an eval-mode stem is not supported")
         N, _, H, W = x.shape
-        dy = dy.to(torch.bfloat16).contiguous(memory_format=_CL)
+        dy = dy.to(ctx.dt).contiguous(memory_format=_CL)
         L = lib()
         dw = gradbuf.out(ctx.pids[0], tuple(wf.shape), x.device)
         dgamma = gradbuf.out(ctx.pids[1], (64,), x.device)
         dbeta = gradbuf.out(ctx.pids[2], (64,), x.device)
         n = L.sqr_stem_fused_workspace_bytes(N, H, W)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(L.sqr_stem_fused_bwd(ptr(x), ctx.xdt, N, H, W, ptr(wf), ptr(gamma), ptr(mean), ptr(invstd), ptr(dy),
+        check(L.sqr_stem_fused_bwd(ptr(x), ctx.xdt, ctx.ydt, N, H, W, ptr(wf), ptr(gamma), ptr(mean), ptr(invstd), ptr(dy),
                                    ptr(y), ptr(arg), ptr(dw), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                    stream_ptr(x.device)), "sqr_stem_fused_bwd")
         gradbuf.written(ctx.pids)
-        return None, dw, dgamma, dbeta, None, None, None, None, None
+        return None, dw, dgamma, dbeta, None, None, None, None, None, None
 
 
 def fused_stem_ok(x, conv, bn):
-    """The fused stem applies: bf16 compute (fp16 takes the unfused conv1 + stem path), 1-channel input that needs no gradient, the resnet18
+    """The fused stem applies: 16-bit compute (bf16 / fp16), 1-channel input that needs no gradient, the resnet18
     conv1 geometry (64 x 1 x 7 x 7, stride 2, pad 3, no bias) and a tileable input size."""
     if not x.is_cuda or x.requires_grad or x.dim() != 4 or x.shape[1] != 1:
         return False
@@ -264,11 +266,11 @@ def fused_stem_ok(x, conv, bn):
     return bool(lib().sqr_stem_fused_supported(x.shape[0], x.shape[2], x.shape[3]))
 
 
-def fused_stem(x, conv, bn, counted=False):
+def fused_stem(x, conv, bn, counted=False, dt=torch.bfloat16):
     training = bn.training or not bn.track_running_stats
     if training and bn.track_running_stats and not counted:
         bn.num_batches_tracked.add_(1)
     mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    return FusedStemFn.apply(x, conv.weight, bn.weight, bn.bias, rm, rv, bool(training), mom, float(bn.eps))
+    return FusedStemFn.apply(x, conv.weight, bn.weight, bn.bias, rm, rv, bool(training), mom, float(bn.eps), dt)

@@ -82,15 +82,16 @@ class ResNet18(nn.Module):
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
             return self.layer4(self.layer3(self.layer2(self.layer1(x))))
         convs = [m for m in self.modules() if isinstance(m, Conv2d)]
-        # bf16: conv1 + bn1 + relu + maxpool as one op that never writes the conv1 activation
-        fuse = x.is_cuda and compute_dtype(x) == torch.bfloat16 and fused_stem_ok(x, self.conv1, self.bn1)
+        # bf16 / fp16: conv1 + bn1 + relu + maxpool as one op that never writes the conv1 activation
+        cdt = compute_dtype(x)
+        fuse = cdt in (torch.bfloat16, torch.float16) and fused_stem_ok(x, self.conv1, self.bn1)
         if fuse:
             convs = [m for m in convs if m is not self.conv1]
         if x.is_cuda:  # pack every conv weight of this step in one launch
             pack_all(convs, compute_dtype(x))
         count_batches([m for m in self.modules() if isinstance(m, nn.BatchNorm2d)])
         if fuse:
-            x = fused_stem(x, self.conv1, self.bn1, counted=True)
+            x = fused_stem(x, self.conv1, self.bn1, counted=True, dt=cdt)
         else:
             x = stem(self.conv1.forward_stats(x, self.bn1), self.bn1, counted=True)  # fused bn1 -> relu -> maxpool
         return self.layer4(self.layer3(self.layer2(self.layer1(x))))

@@ -1,4 +1,4 @@
-"""Fused bf16 stem (libsqr sqr_stem_fused_*: conv1 7x7/2 + bn1 + relu + maxpool(3,2,1), conv1
+"""Fused 16-bit stem (bf16 and fp16; libsqr sqr_stem_fused_*: conv1 7x7/2 + bn1 + relu + maxpool(3,2,1), conv1
 activation never stored) vs torch.nn in float64 on the CPU from the same bf16-rounded input and
 weights, and vs the unfused bf16 libsqr path.
 
@@ -36,32 +36,35 @@ def _mods(seed):
     return conv, bn
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (3, 128, 64), (2, 256, 256)])
-@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16], ids=["xf32", "xbf16"])
-def test_fused_stem_train_matches_torch(N, H, W, xdtype):
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (3, 128, 64), (2, 256, 256), (2, 512, 512)])
+@pytest.mark.parametrize("xdtype,dt", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16),
+                                       (torch.float32, torch.float16), (torch.float16, torch.float16)],
+                         ids=["xf32_bf16", "xbf16_bf16", "xf32_f16", "xf16_f16"])
+def test_fused_stem_train_matches_torch(N, H, W, xdtype, dt):
+    """(2, 512, 512): the config-5 geometry (512x512 input, 256x256 conv1 output)."""
     from sqr.bn import fused_stem, fused_stem_ok
     conv, bn = _mods(N + H)
     g = torch.Generator().manual_seed(H * W)
     x = torch.rand(N, 1, H, W, generator=g)
-    xb = x.bfloat16().float()
-    wb = conv.weight.detach().bfloat16().float()
+    xb = x.to(dt).float()
+    wb = conv.weight.detach().to(dt).float()
     # float64 reference on the bf16-rounded operands, conv output rounded to bf16 like the kernels
     bnr = copy.deepcopy(bn).double().train()
     wr = wb.double().requires_grad_(True)
     c = F.conv2d(xb.double(), wr, stride=2, padding=3)
-    c = c + (c.bfloat16().double() - c).detach()  # bf16 rounding of the stored conv output, identity grad
+    c = c + (c.to(dt).double() - c).detach()  # rounding of the stored conv output, identity grad
     r = F.relu(bnr(c))
-    r = r + (r.bfloat16().double() - r).detach()  # pooled values are bf16: same max-pool ties as the kernel
+    r = r + (r.to(dt).double() - r).detach()  # pooled values are 16-bit: same max-pool ties as the kernel
     yr = F.max_pool2d(r, 3, 2, 1)
-    gy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    gy = torch.randn(yr.shape, generator=g).to(dt).float()
     yr.backward(gy.double())
 
     convg, bng = copy.deepcopy(conv).to(DEV), copy.deepcopy(bn).to(DEV).train()
     xg = x.to(DEV).to(xdtype)
     assert fused_stem_ok(xg, convg, bng)
-    y = fused_stem(xg, convg, bng)
-    assert y.dtype == torch.bfloat16 and y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
-    y.backward(gy.to(DEV).bfloat16().contiguous(memory_format=torch.channels_last))
+    y = fused_stem(xg, convg, bng, dt=dt)
+    assert y.dtype == dt and y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(gy.to(DEV).to(dt).contiguous(memory_format=torch.channels_last))
     torch.cuda.synchronize()
     assert _rel(y, yr) <= 1e-2
     assert _rel(bng.running_mean, bnr.running_mean) <= 1e-3
@@ -71,7 +74,8 @@ def test_fused_stem_train_matches_torch(N, H, W, xdtype):
     assert _rel(bng.bias.grad, bnr.bias.grad) <= 1e-3
 
 
-def test_fused_stem_matches_unfused_bf16_path():
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+def test_fused_stem_matches_unfused_path(dt):
     from sqr import conv as sc
     from sqr.bn import fused_stem, stem
     conv, bn = _mods(3)
@@ -81,10 +85,10 @@ def test_fused_stem_matches_unfused_bf16_path():
         convg, bng = copy.deepcopy(conv).to(DEV), copy.deepcopy(bn).to(DEV).train()
         xg = x.to(DEV)
         if fused:
-            y = fused_stem(xg, convg, bng)
+            y = fused_stem(xg, convg, bng, dt=dt)
         else:
-            y = stem(sc.conv2d(xg.bfloat16(), convg.weight, None, 2, 3, stats=True), bng)
-        gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(2)).to(DEV).bfloat16()
+            y = stem(sc.conv2d(xg.to(dt), convg.weight, None, 2, 3, stats=True), bng)
+        gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(2)).to(DEV).to(dt)
         y.backward(gy.contiguous(memory_format=torch.channels_last))
         res.append((y.float(), convg.weight.grad, bng.weight.grad, bng.bias.grad, bng.running_var.clone()))
     for a, b in zip(*res):
