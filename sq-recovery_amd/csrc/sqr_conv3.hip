@@ -1093,19 +1093,19 @@ namespace {
 bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) {
   if (K % 64 || C % 64) return false;
   *nch = K / 64;
-  if (Wo == 32 && Ho % 8 == 0 && C == 64 && K == 128) {  // layer 2 (tiles must match the launches below)
-    *TH = 8; *TW = 32; *BN = 64;
-    return true;
+  *BN = 64;
+  // tile per channel geometry (the launches below are instantiated for these); any image size the
+  // tile divides (256x256 input: layer 2 / 3 / 4 = 32 / 16 / 8 wide, 512x512: 64 / 32 / 16)
+  if (C == 64 && K == 128) {  // layer 2
+    *TH = 8; *TW = 32;
+  } else if (C == 128 && K == 256) {  // layer 3
+    *TH = 4; *TW = 16;
+  } else if (C == 256 && K == 512) {  // layer 4
+    *TH = 8; *TW = 8;
+  } else {
+    return false;
   }
-  if (Wo == 16 && Ho % 8 == 0 && C == 128 && K == 256) {  // layer 3
-    *TH = 4; *TW = 16; *BN = 64;
-    return true;
-  }
-  if (Wo == 8 && Ho % 8 == 0 && C == 256 && K == 512) {  // layer 4
-    *TH = 8; *TW = 8; *BN = 64;
-    return true;
-  }
-  return false;
+  return Wo % *TW == 0 && Ho % *TH == 0;
 }
 }  // namespace
 

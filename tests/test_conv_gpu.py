@@ -206,7 +206,9 @@ def test_conv3_persistent_bands(N):
 
 
 @pytest.mark.parametrize("shape", [(2, 64, 64, 128), (3, 128, 32, 256), (3, 256, 16, 512), (64, 64, 64, 128),
-                                   (64, 128, 32, 256), (64, 256, 16, 512)],
+                                   (64, 128, 32, 256), (64, 256, 16, 512),
+                                   (2, 64, 128, 128), (2, 128, 64, 256), (2, 256, 32, 512),  # 512x512 input
+                                   (16, 64, 128, 128), (16, 128, 64, 256), (16, 256, 32, 512)],
                          ids=lambda s: "N%dC%dH%dK%d" % s)
 def test_conv3s2_dgrad_direct(shape):
     """Direct stride-2 backward-data kernel (layers 2-4 first convs: all four parity classes in one

@@ -13,7 +13,7 @@ timeout -k 10 300 python -u bench.py --cpu-steps 0 "$@" > "$OUT/bench.json" 2> "
 cat "$OUT/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o prof -- \
   python -u bench.py --steps 20 --warmup 5 --profile "$@" > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err"
-python tools/step_stats.py "$OUT/prof" 20 > "$OUT/steps.txt"
+python tools/step_stats.py "$OUT/prof" 20 "$OUT/seq.txt" > "$OUT/steps.txt"
 find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 rm -rf "$OUT/prof"
 head -45 "$OUT/steps.txt"

@@ -7,7 +7,10 @@ of the fp16 configuration, else the optimizer's crsk_kernel).  Prints the per-st
 wall span per step (first kernel start to last kernel end, over the STEPS steps) and one line per
 kernel: us/step, launches/step, average us.
 
-    python tools/step_stats.py gpurun_out/TAG/prof STEPS [> profiles/rNN_..._steps.txt]
+    python tools/step_stats.py gpurun_out/TAG/prof STEPS [SEQ_FILE] [> profiles/rNN_..._steps.txt]
+
+With SEQ_FILE, also writes the launch sequence of the last timed step there: per launch its start
+offset, duration (us) and kernel name (per-layer attribution of the aggregated lines).
 """
 import collections
 import csv
@@ -48,6 +51,12 @@ def main():
           % (steps, len(sel) / steps, total / steps / 1e3, span / steps / 1e3, end_marker))
     for k, (t, c) in sorted(per.items(), key=lambda kv: -kv[1][0]):
         print("%8.1f us/step %6.2f calls/step %8.2f us avg  %s" % (t / steps / 1e3, c / steps, t / c / 1e3, k))
+    if len(sys.argv) > 3:
+        last = rows[ends[-2] + 1:ends[-1] + 1]
+        t0 = last[0][0]
+        with open(sys.argv[3], "w") as f:
+            for i, (s, e, n) in enumerate(last):
+                f.write("%4d %9.1f %8.2f  %s\n" % (i, (s - t0) / 1e3, (e - s) / 1e3, short(n)))
 
 
 if __name__ == "__main__":
