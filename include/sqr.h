@@ -164,6 +164,12 @@ int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_c
  * launch; bf16 3x3/s2 shapes of ResNetSQ's layers 2-4 take the direct window kernel instead. */
 int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
                         void* workspace, size_t workspace_bytes, void* stream);
+/* dx = bwd_data(dy) + addend (addend [N,H,W,C] in the conv dtype, distinct from dx): the gradient
+ * of a residual block's input, whose identity / downsample branch contributes `addend`
+ * (torchvision BasicBlock `out += identity`, torch/models.py:181).  The direct 3x3 kernels add in
+ * their epilogues (the sum is never a separate pass); other shapes add after the GEMM. */
+int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void* dx, const void* addend,
+                            const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
 /* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
 int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                           void* workspace, size_t workspace_bytes, void* stream);

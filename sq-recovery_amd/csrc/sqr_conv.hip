@@ -1162,26 +1162,73 @@ static DgradClass dgrad_class(const sqr_conv_desc* d, int ph, int pw) {
   return c;
 }
 
-extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
-                                   void* workspace, size_t workspace_bytes, void* stream) {
-  (void)workspace;
-  (void)workspace_bytes;
+static int bwd_data_gemm(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d, const Shape& sh,
+                         hipStream_t st);
+
+// dx += addend over n elements (the implicit-GEMM backward-data path of sqr_conv2d_bwd_data_acc;
+// the direct kernels add in their epilogues)
+template <typename T>
+__global__ void __launch_bounds__(256) add_inplace_kernel(T* __restrict__ dx, const T* __restrict__ addend, long long n) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dx[i + e] = (T)((float)dx[i + e] + (float)addend[i + e]);
+  } else {
+    for (long long e = i; e < n; ++e) dx[e] = (T)((float)dx[e] + (float)addend[e]);
+  }
+}
+
+static int bwd_data_impl(const void* dy, const void* w_crsk, void* dx, const void* addend, const sqr_conv_desc* d,
+                         void* stream) {
   Shape sh;
   int rc = check_desc(d, &sh);
   if (rc) return rc;
   SQR_CHECK_ARG(!sh.im2col, "conv2d_bwd_data: C=%d < 8 not supported", d->C);
   SQR_CHECK_ARG(dy && w_crsk && dx, "conv2d_bwd_data: null pointer");
+  SQR_CHECK_ARG(addend != dx, "conv2d_bwd_data_acc: addend must not alias dx");
   hipStream_t st = as_stream(stream);
   if (direct3(d, sh)) {
-    rc = conv3_launch(d->dtype, dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, st);
+    rc = conv3_launch(d->dtype, dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, st, addend);
     if (rc != kNotHandled) return rc;
   }
   if (d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->stride == 2 && d->pad == 1 &&
       d->H == 2 * sh.Ho && d->W == 2 * sh.Wo) {
     const int off[4] = {0, d->C * d->K, 3 * d->C * d->K, 5 * d->C * d->K};  // classes of 1, 2, 2, 4 taps
-    rc = conv3s2_dgrad_launch(d->dtype, dy, w_crsk, off, dx, d->N, sh.Ho, sh.Wo, d->K, d->C, st);
+    rc = conv3s2_dgrad_launch(d->dtype, dy, w_crsk, off, dx, d->N, sh.Ho, sh.Wo, d->K, d->C, st, addend);
     if (rc != kNotHandled) return rc;
   }
+  rc = bwd_data_gemm(dy, w_crsk, dx, d, sh, st);
+  if (rc || !addend) return rc;
+  const long long n = (long long)d->N * d->H * d->W * d->C;
+  const unsigned grid = (unsigned)((n + 1023) / 1024);
+  if (d->dtype == SQR_DTYPE_F32)
+    hipLaunchKernelGGL(add_inplace_kernel<float>, dim3(grid), dim3(256), 0, st, (float*)dx, (const float*)addend, n);
+  else
+    SQR_DISPATCH16(d->dtype, T, hipLaunchKernelGGL(add_inplace_kernel<T>, dim3(grid), dim3(256), 0, st, (T*)dx,
+                                                   (const T*)addend, n));
+  SQR_HIP_LAUNCH_CHECK("add_inplace_kernel");
+  return 0;
+}
+
+extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  return bwd_data_impl(dy, w_crsk, dx, nullptr, d, stream);
+}
+
+extern "C" int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void* dx, const void* addend,
+                                       const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  SQR_CHECK_ARG(addend, "conv2d_bwd_data_acc: null addend");
+  return bwd_data_impl(dy, w_crsk, dx, addend, d, stream);
+}
+
+// implicit-GEMM backward-data over the output parity classes
+static int bwd_data_gemm(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d, const Shape& sh,
+                         hipStream_t st) {
+  int rc = 0;
   // dX[n,h,w,c] = sum_{r,s,k} dY[n,(h+p-r)/st,(w+p-s)/st,k] W[k,c,r,s] over the divisible taps.
   // Output pixels split by parity (h%st, w%st); in class (ph,pw) only taps r = r0 + st*t contribute
   // and dY row = i + off_h - t: a stride-1 implicit GEMM over the class grid (Hc x Wc).

@@ -41,6 +41,7 @@ struct D3Args {
   const void* x;    // [N][H][W][Cin]
   const void* w;    // [Nout][9][Cin]
   void* out;        // [N][H][W][Nout]
+  const void* addend;  // nullable: out = conv + addend ([N][H][W][Nout], may alias out)
   float* stats;     // nullable: BatchNorm partials [ntm][2][Nout]
   int N, H, W, Cin, Nout;
   int tiles_x, tiles_per_img;
@@ -123,7 +124,11 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 // (small late-layer images: more pixels per weight tile fetched)
 // PD: weight tiles prefetched ahead (ring of PD + 1 stages): the per-CU LDS-DMA delivery is
 // latency x bytes-in-flight bound, so deeper rings buy throughput where LDS allows
-template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2>
+// ACC (backward-data of a block input): out = conv + a.addend.  The addend is loaded into registers
+// before the first DMA of the kernel, so its HBM read overlaps the main loop instead of adding a
+// burst at the end (measured at B=64: +3.9 us on layer 2 when read in the epilogue).
+template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2,
+          bool ACC = false>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
   constexpr int ROWB = 128, STAGES = PD + 1;
@@ -152,6 +157,24 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   const int ty = trem / a.tiles_x, tx = trem - ty * a.tiles_x;
   const int h0 = ty * TH, w0 = tx * TW, n0 = tile_n * BN;
 
+  // output element offset of this lane's pixel i, channels n0 + wn*WN + 4fq (+ 16 j)
+  const int fr = lane & 15, fq = lane >> 4;
+  auto out_off = [&](int i) -> size_t {
+    const int m = wm * WM + 16 * i + fr;
+    const int ii = m / (TH * TW), mm = m - ii * (TH * TW);
+    return (((size_t)(img + ii) * a.H + h0 + mm / TW) * a.W + w0 + (mm % TW)) * a.Nout + n0 + wn * WN + 4 * fq;
+  };
+  u32x2 av[ACC ? TN : 1][ACC ? TM : 1];
+  if constexpr (ACC) {
+    const uint16_t* ad = (const uint16_t*)a.addend;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const size_t o = out_off(i);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) av[j][i] = *(const u32x2*)(ad + o + 16 * j);
+    }
+  }
+
   // ---- per-lane DMA offsets (fixed for the whole kernel; chunk / tap parts are scalar)
   constexpr uint32_t kOOB = 0x80000000u;
   const int prow = lane >> 3, pslot = lane & 7;
@@ -177,7 +200,6 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   const __amdgpu_buffer_rsrc_t wsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, a.wbytes, 0x00020000);
 
   // ---- fragment coordinates
-  const int fr = lane & 15, fq = lane >> 4;
   int qbase[TM];  // window row of this lane's output pixel at tap shift (0, 0)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -312,7 +334,22 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     __builtin_amdgcn_s_barrier();
   }
 
-  // ---- epilogue: lane holds out[pixel m][n..n+3]; convert once, store, then BN partials
+  // ---- epilogue: lane holds out[pixel m][n..n+3]; convert once (ACC: after adding the addend),
+  // store, then BN partials
+  size_t opix[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) opix[i] = out_off(i);
+  if constexpr (ACC) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        acc[j][i][0] += lo2f<T>(av[j][i][0]);
+        acc[j][i][1] += hi2f<T>(av[j][i][0]);
+        acc[j][i][2] += lo2f<T>(av[j][i][1]);
+        acc[j][i][3] += hi2f<T>(av[j][i][1]);
+      }
+  }
   uint32_t pk[TN][TM][2];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -321,16 +358,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       pk[j][i][0] = pack2<T>(acc[j][i][0], acc[j][i][1]);
       pk[j][i][1] = pack2<T>(acc[j][i][2], acc[j][i][3]);
     }
-  uint16_t* __restrict__ out = (uint16_t*)a.out;
+  uint16_t* out = (uint16_t*)a.out;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wm * WM + 16 * i + fr;
-    const int ii = m / (TH * TW), mm = m - ii * (TH * TW);
-    const size_t pix = ((size_t)(img + ii) * a.H + h0 + mm / TW) * a.W + w0 + (mm % TW);
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      *(u32x2*)(out + pix * a.Nout + n0 + wn * WN + 16 * j + 4 * fq) = u32x2{pk[j][i][0], pk[j][i][1]};
-  }
+    for (int j = 0; j < TN; ++j) *(u32x2*)(out + opix[i] + 16 * j) = u32x2{pk[j][i][0], pk[j][i][1]};
   if (a.stats)
     tile_stats<T, BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
                                                  a.stats + ((size_t)tile_m * 2) * a.Nout + n0,
@@ -353,6 +385,7 @@ struct D3PArgs {
   const void* x;   // [N][H][64][64]
   const void* w;   // [64][9][64]
   void* out;       // [N][H][64][64]
+  const void* addend;  // ACC launches: out = conv + addend (backward-data of a block input; may alias out)
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
   int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
@@ -369,13 +402,20 @@ __device__ __forceinline__ void wait_vm(int n) {
     case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
 // STATS: the forward's BatchNorm partials (a.stats != NULL); the backward-data launches skip the
-// per-tile accumulation entirely (it cost ~0.15 us per tile)
-template <typename T, bool STATS>
+// per-tile accumulation entirely (it cost ~0.15 us per tile).
+// ACC (backward-data): out = conv + addend.  The addend of tile k is loaded into registers at the
+// start of iteration k (16-B pieces in the staged-store layout) and added when tile k is stored
+// at the start of iteration k+1, so its latency hides behind a whole tile of MFMA work; to keep
+// the compiler's wait for those registers from also waiting on just-issued row loads, ACC
+// launches store the previous tile BEFORE issuing the next rows.
+template <typename T, bool STATS, bool ACC = false>
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
   // 2 x 2 waves, each 64 pixels (one image row) x 32 channels = two 32x32 MFMA accumulators
@@ -454,12 +494,23 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) st1[e] = st2[e] = 0.f;
 
+  u32x4 av[NST];  // ACC: the addend pieces of the tile stored next
+  auto load_addend = [&](int k) {
+    const char* src = (const char*)a.addend + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
+#pragma unroll
+    for (int q = 0; q < NST; ++q) av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
+  };
   auto store_staged = [&](int k) {
-    char* __restrict__ dst = (char*)a.out + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
+    char* dst = (char*)a.out + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
 #pragma unroll
     for (int q = 0; q < NST; ++q) {
       const int c = q * NT + tid, row = c >> 3, slot = c & 7;
-      const u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
+      u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
+      if constexpr (ACC) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = pack2<T>(lo2f<T>(v[e]) + lo2f<T>(av[q][e]), hi2f<T>(v[e]) + hi2f<T>(av[q][e]));
+      }
 #if SQR_EXP & 256
       if (v[0] == 0x12345678u && v[1] == 0x9abcdef0u) *(u32x4*)(dst + (size_t)c * 16) = v;
 #else
@@ -475,12 +526,19 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 
   for (int k = 0; k < ntile; ++k) {
     // tile k+2's new rows go into the slots tile k-1 used (free since the last barrier)
+    int pn;
+    if constexpr (ACC) {
+      if (k >= 1) store_staged(k - 1);
+      pn = k + 2 < ntile ? issue_rows(hb + 2 * (k + 2) + 1, 2) : 0;
+      load_addend(k);
+    } else {
 #if SQR_EXP & 512
-    const int pn = 0;
+      pn = 0;
 #else
-    const int pn = k + 2 < ntile ? issue_rows(hb + 2 * (k + 2) + 1, 2) : 0;
+      pn = k + 2 < ntile ? issue_rows(hb + 2 * (k + 2) + 1, 2) : 0;
 #endif
-    if (k >= 1) store_staged(k - 1);
+      if (k >= 1) store_staged(k - 1);
+    }
     f32x16 acc[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -549,8 +607,12 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 #endif
       }
     // tile k+1's rows (issued one iteration ago) have landed; younger in this wave's queue: the
-    // stores of tile k-2, the row loads of tile k+2 and the stores of tile k-1
-    wait_vm(pn + (k >= 1 ? NST : 0) + (k >= 2 ? NST : 0));
+    // stores of tile k-2, the row loads of tile k+2 and the stores of tile k-1 (ACC: the addend
+    // loads of tile k-1, the stores of tile k-1, the row loads of tile k+2, the addend loads of k)
+    if constexpr (ACC)
+      wait_vm(pn + (k >= 1 ? 2 * NST : 0) + NST);
+    else
+      wait_vm(pn + (k >= 1 ? NST : 0) + (k >= 2 ? NST : 0));
     __builtin_amdgcn_s_barrier();  // ... for every wave; all waves are done with tile k's rows and the staging area
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -604,10 +666,12 @@ struct D3S2Args {
   const void* dy;  // [N][Ho][Wo][K]
   const void* w;   // parity classes back to back, class cl = [C][Rc][Sc][K]
   void* dx;        // [N][2Ho][2Wo][C]
+  const void* addend;  // nullable: dx = dgrad + addend (may alias dx)
   int N, Ho, Wo, K, C;
   int tiles_x, tiles_per_img, ntn;
   int cls_off[4];  // elements
   uint32_t dybytes, wbytes;
+  unsigned long long* tp;  // nullable: clock probe slots
 };
 
 __host__ __device__ constexpr int s2_ntaps(int cl) { return (1 + (cl >> 1)) * (1 + (cl & 1)); }
@@ -628,6 +692,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   static_assert(PD <= 8, "the next window must land within its chunk's 9 steps");
   __shared__ __attribute__((aligned(1024))) char smem[NWIN * WIN + STAGES * TILE_B];
   char* const bring = smem + NWIN * WIN;
+  clock_begin(a.tp);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -769,9 +834,32 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   }
   static_assert(SL >= 8, "staging swizzle assumes at least 8 slots per pixel");
   const int H = 2 * a.Ho, W = 2 * a.Wo;
-  T* __restrict__ out = (T*)a.dx;
+  T* out = (T*)a.dx;
+  // copy-out: 16-B pieces of contiguous dX rows (+ the addend's pieces, AG at a time: the 8-wave
+  // layer-2 kernel has no registers to spare).  A half's first addend group is requested before
+  // its staging writes so that its latency overlaps them.
+  constexpr int NIT = (HALF + 64 * NW - 1) / (64 * NW), AG = NIT < 4 ? NIT : 4;
+  static_assert(NIT % AG == 0, "addend groups");
+  auto piece = [&](int it, int ph, int& p, int& sl, size_t& go) {
+    const int idx = tid + it * 64 * NW;
+    p = idx / SL;
+    sl = idx - p * SL;
+    const int y = p / PX, x = p - y * PX;
+    go = (((size_t)img * H + 2 * (i0 + y) + ph) * W + 2 * j0 + x) * a.C + n0 + 8 * sl;
+    return idx < HALF && i0 + y < a.Ho && j0 + (x >> 1) < a.Wo;
+  };
+  auto load_group = [&](int it0, int ph, uint4* av) {
+#pragma unroll
+    for (int u = 0; u < AG; ++u) {
+      int p, sl;
+      size_t go;
+      if (piece(it0 + u, ph, p, sl, go)) av[u] = *(const uint4*)((const T*)a.addend + go);
+    }
+  };
 #pragma unroll
   for (int ph = 0; ph < 2; ++ph) {
+    uint4 av[AG];
+    if (a.addend) load_group(0, ph, av);
     if (ph) __syncthreads();  // previous half copied out
 #pragma unroll
     for (int pw = 0; pw < 2; ++pw)
@@ -790,19 +878,31 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
         }
       }
     __syncthreads();
-    for (int idx = tid; idx < HALF; idx += 64 * NW) {
-      const int p = idx / SL, sl = idx - p * SL;
-      const int y = p / PX, x = p - y * PX;
-      if (i0 + y >= a.Ho || j0 + (x >> 1) >= a.Wo) continue;
-      const uint4 v = *(const uint4*)(smem + p * (BN * 2) + ((sl ^ ((p >> 1) & 7)) << 4));
-      const size_t pix = ((size_t)img * H + 2 * (i0 + y) + ph) * W + 2 * j0 + x;
+#pragma unroll
+    for (int it0 = 0; it0 < NIT; it0 += AG) {
+      if (it0 && a.addend) load_group(it0, ph, av);
+#pragma unroll
+      for (int u = 0; u < AG; ++u) {
+        int p, sl;
+        size_t go;
+        if (!piece(it0 + u, ph, p, sl, go)) continue;
+        uint4 v = *(const uint4*)(smem + p * (BN * 2) + ((sl ^ ((p >> 1) & 7)) << 4));
+        if (a.addend) {
+          uint32_t* vv = (uint32_t*)&v;
+          const uint32_t* aa = (const uint32_t*)&av[u];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            vv[e] = pack2<T>(lo2f<T>(vv[e]) + lo2f<T>(aa[e]), hi2f<T>(vv[e]) + hi2f<T>(aa[e]));
+        }
 #if SQR_EXP & 2048
-      if (v.x == 12345u)
+        if (v.x == 12345u)
 #endif
-      *(uint4*)(out + pix * a.C + n0 + 8 * sl) = v;
+        *(uint4*)(out + go) = v;
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail loads
+  clock_end(a.tp);
 }
 
 // ============================================================================ weight gradient
@@ -1110,7 +1210,7 @@ bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) 
 }  // namespace
 
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,
-                         int Wo, int K, int C, hipStream_t st) {
+                         int Wo, int K, int C, hipStream_t st, const void* addend) {
   if (g_direct == 0) return kNotHandled;
   int TH, TW, BN, nch;
   if (!s2_pick(Ho, Wo, K, C, &TH, &TW, &BN, &nch)) return kNotHandled;
@@ -1120,6 +1220,7 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
   a.dy = dy;
   a.w = w_cls;
   a.dx = dx;
+  a.addend = addend;
   a.N = N;
   a.Ho = Ho;
   a.Wo = Wo;
@@ -1131,6 +1232,7 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
   for (int i = 0; i < 4; ++i) a.cls_off[i] = cls_off[i];
   a.dybytes = (uint32_t)dybytes;
   a.wbytes = (uint32_t)wbytes;
+  a.tp = probe_clock_take();
   // measured (N=64, rocprofv3): layer 2 17.9 us (8x32 tile, 5-deep weight ring, 8 waves), layer 3
   // 17.6 us (4x16 tile, two workgroups per CU), layer 4 20.0 us (one 8x8 image per tile; the
   // implicit GEMM: 39.6 / 23.2 / 23.7 us); 4x32 / 8x16 / BN 128 / 2x2-wave / deeper-ring variants were
@@ -1153,7 +1255,7 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
 
 // kNotHandled = not applicable (caller falls back to the implicit-GEMM path), 0 = launched, else error
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
-                 float* stats, int* stats_rows, hipStream_t st) {
+                 float* stats, int* stats_rows, hipStream_t st, const void* addend) {
   if (g_direct == 0) return kNotHandled;
   if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return kNotHandled;
   const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
@@ -1174,6 +1276,7 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     p.x = x;
     p.w = w;
     p.out = out;
+    p.addend = addend;
     p.stats = stats;
     p.H = H;
     p.bpi = bpi;
@@ -1188,6 +1291,8 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     SQR_DISPATCH16(dtype, T, {
       if (stats)
         hipLaunchKernelGGL((conv3p_kernel<T, true>), dim3(grid), dim3(256), 0, st, p);
+      else if (addend)
+        hipLaunchKernelGGL((conv3p_kernel<T, false, true>), dim3(grid), dim3(256), 0, st, p);
       else
         hipLaunchKernelGGL((conv3p_kernel<T, false>), dim3(grid), dim3(256), 0, st, p);
     });
@@ -1201,6 +1306,7 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   a.x = x;
   a.w = w;
   a.out = out;
+  a.addend = addend;
   a.stats = stats;
   a.N = N;
   a.H = H;
@@ -1218,21 +1324,28 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   if (stats_rows) *stats_rows = a.ntm;
   const dim3 grid(a.ntm * a.ntn), blk(c.threads);
   probe_begin(st);
+#define SQR_D3_CASES(ACC_)                                                                                         \
+  switch (c.id) {                                                                                                  \
+    case 0: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 64, 4, 1, 1, 2, ACC_>), grid, blk, 0, st, a); break;    \
+    case 1: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;   \
+    case 2: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;   \
+    case 3: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;     \
+    case 4: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 16, 16, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;   \
+    case 5: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 2, ACC_>), grid, blk, 0, st, a); break;     \
+    case 6: hipLaunchKernelGGL((conv3_kernel<T, 256, 32, 4, 1, 8, 8, 2, 4, 2, ACC_>), grid, blk, 0, st, a); break;     \
+    case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 3, ACC_>), grid, blk, 0, st, a); break;   \
+    case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5, ACC_>), grid, blk, 0, st, a); break;   \
+    case 9: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 5, ACC_>), grid, blk, 0, st, a); break;     \
+    default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8, ACC_>), grid, blk, 0, st, a); break;    \
+  }
   SQR_DISPATCH16(dtype, T, {
-    switch (c.id) {
-      case 0: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 64, 4, 1>), grid, blk, 0, st, a); break;
-      case 1: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2>), grid, blk, 0, st, a); break;
-      case 2: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2>), grid, blk, 0, st, a); break;
-      case 3: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2>), grid, blk, 0, st, a); break;
-      case 4: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 16, 16, 2>), grid, blk, 0, st, a); break;
-      case 5: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2>), grid, blk, 0, st, a); break;
-      case 6: hipLaunchKernelGGL((conv3_kernel<T, 256, 32, 4, 1, 8, 8, 2, 4>), grid, blk, 0, st, a); break;
-      case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 3>), grid, blk, 0, st, a); break;
-      case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5>), grid, blk, 0, st, a); break;
-      case 9: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 5>), grid, blk, 0, st, a); break;
-      default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8>), grid, blk, 0, st, a); break;
+    if (addend) {
+      SQR_D3_CASES(true)
+    } else {
+      SQR_D3_CASES(false)
     }
   });
+#undef SQR_D3_CASES
   probe_end(st);
   SQR_HIP_LAUNCH_CHECK("conv3_kernel");
   return 0;

@@ -152,12 +152,13 @@ constexpr int kNotHandled = -1000;
 
 // direct 3x3/s1/p1 bf16 / fp16 kernel (sqr_conv3.hip): kNotHandled = shape not handled (use the
 // implicit-GEMM path), 0 = launched, otherwise an error code
+// addend (nullable, backward-data only): out = conv + addend, fused into the epilogue
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
-                 float* stats, int* stats_rows, hipStream_t st);
+                 float* stats, int* stats_rows, hipStream_t st, const void* addend = nullptr);
 // direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,
-                         int Wo, int K, int C, hipStream_t st);
+                         int Wo, int K, int C, hipStream_t st, const void* addend = nullptr);
 // direct 3x3/s1/p1 bf16 weight gradient: fp32 slabs [splits][K][9*C] ((tap, c) columns, the
 // implicit-GEMM TN layout) for wgrad_reduce_kernel.  conv3w_slab_bytes = 0 if not handled.
 size_t conv3w_slab_bytes(int N, int H, int W, int C, int K);

@@ -74,6 +74,8 @@ SIGNATURES = {
                                      ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                     c_size_t, c_void_p]),
+    "sqr_conv2d_bwd_data_acc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),
+                                        c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                       c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight_col": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,

@@ -35,7 +35,8 @@ def _ws_bytes(M, C):
 
 class BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps, stats=None):
+    def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps, stats=None,
+                res_join=None):
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
@@ -63,6 +64,7 @@ class BNActFn(torch.autograd.Function):
                                    stream_ptr(x.device)), "sqr_bn_fwd")
         ctx.relu, ctx.training, ctx.eps = relu, training, eps
         ctx.has_res = residual is not None
+        ctx.res_join = res_join  # sqr.conv.ResidualJoin of the residual input: its gradient is deposited
         ctx.pids = (id(weight), id(bias))
         if training:
             ctx.save_for_backward(x, mask, weight, mean, invstd)
@@ -82,7 +84,9 @@ class BNActFn(torch.autograd.Function):
             xhat = (x.float() - m.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
             dx = (g * (weight * invstd).view(1, C, 1, 1)).to(x.dtype)
             dres = g.to(x.dtype) if ctx.has_res else None
-            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None
+            if ctx.res_join is not None:
+                dres = ctx.res_join.deposit(dres)
+            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None, None
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
         dgamma = gradbuf.out(ctx.pids[0], (C,), x.device)
@@ -95,7 +99,9 @@ class BNActFn(torch.autograd.Function):
         gradbuf.written(ctx.pids)
         if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
             dres = dy
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None
+        if ctx.res_join is not None:
+            dres = ctx.res_join.deposit(dres)
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
 
 
 def count_batches(bns):
@@ -121,10 +127,11 @@ def _check_stats(stats, x):
     return stats
 
 
-def bn_act(x, bn, residual=None, relu=True, counted=False):
+def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None):
     """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics.
     x may be a (y, partials) pair from a stats-producing conv: training mode then takes the batch
-    statistics from the partials instead of reducing over y."""
+    statistics from the partials instead of reducing over y.  res_join: the residual input's
+    sqr.conv.ResidualJoin (its gradient goes there instead of to autograd)."""
     x, stats = _split(x)
     training = bn.training or not bn.track_running_stats
     if training and bn.track_running_stats and not counted:
@@ -133,7 +140,7 @@ def bn_act(x, bn, residual=None, relu=True, counted=False):
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
-                         _check_stats(stats, x))
+                         _check_stats(stats, x), res_join if residual is not None else None)
 
 
 class StemFn(torch.autograd.Function):

@@ -235,6 +235,61 @@ def conv2d_bwd_weight(x, gy, d, col=None, wid=None):
     return dw
 
 
+def conv2d_bwd_data_acc(gy, w_crsk, d, addend):
+    """bwd_data(gy) + addend in one pass (sqr_conv2d_bwd_data_acc: the direct kernels add in their
+    epilogues)."""
+    import ctypes
+    dt = _TORCH_DT[d.dtype]
+    dx = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=gy.device, memory_format=_CL)
+    ws, n = _ws(d, 1, gy.device)
+    with _Probe("dgrad", d):
+        rc = lib().sqr_conv2d_bwd_data_acc(ptr(gy), ptr(w_crsk), ptr(dx), ptr(addend), ctypes.byref(d), ptr(ws), n,
+                                           stream_ptr(gy.device))
+    check(rc, "sqr_conv2d_bwd_data_acc")
+    return dx
+
+
+class ResidualJoin:
+    """The two gradient contributions of a residual block's input x (torchvision BasicBlock:
+    x feeds conv1 AND the identity / downsample branch, torch/models.py:181) summed without a
+    separate add pass: the branch op (the identity's BatchNorm residual input, or the downsample
+    conv) DEPOSITS its gradient here instead of returning it to autograd, and conv1's backward-data
+    adds it in its epilogue (sqr_conv2d_bwd_data_acc).  Whichever order autograd runs the two
+    in, the total is right: a deposit made after conv1's backward already ran is returned to
+    autograd as usual (which then adds it)."""
+
+    __slots__ = ("pending", "acc_done")
+
+    def __init__(self):
+        self.pending = None
+        self.acc_done = False
+
+    @staticmethod
+    def make(x):
+        """A join for block input x, or None where it does not apply (CPU, no grad, fp32)."""
+        if (x.is_cuda and x.requires_grad and torch.is_grad_enabled() and x.dim() == 4
+                and x.dtype in (torch.bfloat16, torch.float16) and compute_dtype(x) == x.dtype):
+            return ResidualJoin()
+        return None
+
+    def deposit(self, g):
+        """Branch side: the gradient to return to autograd (None when deposited)."""
+        if g is None:
+            return None
+        if self.acc_done:  # conv1's backward already ran: autograd adds this one
+            self.acc_done = False
+            return g
+        self.pending = g
+        return None
+
+    def take(self):
+        """conv1 side: the deposited gradient (or None: conv1 runs first, the branch returns its own)."""
+        g, self.pending = self.pending, None
+        if g is None:
+            self.acc_done = True
+        return g
+
+
 def compute_dtype(x):
     if x.dtype in (torch.bfloat16, torch.float16):
         return x.dtype
@@ -247,7 +302,7 @@ def compute_dtype(x):
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False):
+    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False, join=None, role=None):
         # the statistics output is non-differentiable: don't let autograd materialise a zero
         # gradient tensor for it in backward
         ctx.set_materialize_grads(False)
@@ -268,6 +323,7 @@ class Conv2dFn(torch.autograd.Function):
         if bias is not None:
             y = y + bias.to(dt).view(1, K, 1, 1)
         ctx.d = d
+        ctx.join, ctx.role = join, role  # ResidualJoin of x: role "acc" (conv1) / "dep" (downsample)
         ctx.wid = id(weight)
         ctx.x_dtype = x.dtype
         ctx.has_bias = bias is not None
@@ -283,7 +339,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, *_):
         if gy is None:  # grads are not materialised (see forward)
-            return None, None, None, None, None, None, None, None
+            return (None,) * 10
         xin, crsk, col = ctx.saved_tensors
         d = ctx.d
         dt = _TORCH_DT[d.dtype]
@@ -292,22 +348,33 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if crsk is None:
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
-            dx = conv2d_bwd_data(g, crsk, d).to(ctx.x_dtype)
+            addend = ctx.join.take() if (ctx.join is not None and ctx.role == "acc") else None
+            if addend is not None and addend.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W) \
+                    and addend.is_contiguous(memory_format=_CL):
+                dx = conv2d_bwd_data_acc(g, crsk, d, addend)
+            else:
+                dx = conv2d_bwd_data(g, crsk, d)
+                if addend is not None:
+                    dx = dx + addend
+            dx = dx.to(ctx.x_dtype)
+            if ctx.join is not None and ctx.role == "dep":
+                dx = ctx.join.deposit(dx)
         if ctx.needs_input_grad[1]:
             dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid)
             gradbuf.written((ctx.wid,))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False):
+def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False, join=None, role=None):
     """conv(x); with stats=True returns (y, partials) where partials feed the following
     BatchNorm (sqr.bn.bn_act / stem ``stats=``) so it skips its statistics pass over y
     (partials is None when the conv has a bias)."""
     if not x.is_cuda:
         raise ValueError("sqr conv2d runs on MI355X; got a %s tensor" % x.device)
-    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed, bool(stats))
+    return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed, bool(stats), join,
+                          role)
 
 
 class Conv2d(nn.Conv2d):
@@ -334,9 +401,12 @@ class Conv2d(nn.Conv2d):
             return super().forward(x)
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x))
 
-    def forward_stats(self, x, bn=None):
+    def forward_stats(self, x, bn=None, join=None, role=None):
         """(y, BatchNorm partials of y) — see conv2d(stats=True).  With `bn` given, the partials
-        are produced only when that BatchNorm will use batch statistics (else y alone)."""
-        if not x.is_cuda or (bn is not None and not (bn.training or not bn.track_running_stats)):
+        are produced only when that BatchNorm will use batch statistics (else y alone).  join/role:
+        a ResidualJoin of x (see there)."""
+        if not x.is_cuda:
             return self.forward(x)
-        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x), stats=True)
+        want = bn is None or bn.training or not bn.track_running_stats
+        return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x), stats=want,
+                      join=join, role=role)

@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from .bn import bn_act, count_batches, fused_stem, fused_stem_ok, stem
-from .conv import Conv2d, compute_dtype, pack_all
+from .conv import Conv2d, ResidualJoin, compute_dtype, pack_all
 
 
 class BasicBlock(nn.Module):
@@ -35,13 +35,18 @@ class BasicBlock(nn.Module):
             out = self.bn2(self.conv2(self.relu(self.bn1(self.conv1(x)))))
             return self.relu(out + identity)
         # conv -> fused [bn+relu] -> conv -> fused [bn + identity + relu]   (libsqr kernels)
-        # (training: each conv's epilogue also emits the batch statistics its BN needs)
-        out = bn_act(self.conv1.forward_stats(x, self.bn1), self.bn1, relu=True, counted=True)
-        identity = x
+        # (training: each conv's epilogue also emits the batch statistics its BN needs; backward:
+        # the identity / downsample branch's gradient of x is added in conv1's backward-data
+        # epilogue through a ResidualJoin instead of a separate add)
+        join = ResidualJoin.make(x)
+        out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc"), self.bn1, relu=True, counted=True)
+        identity, res_join = x, join
         if self.downsample is not None:
-            identity = bn_act(self.downsample[0].forward_stats(x, self.downsample[1]),
+            identity = bn_act(self.downsample[0].forward_stats(x, self.downsample[1], join=join, role="dep"),
                               self.downsample[1], relu=False, counted=True)
-        return bn_act(self.conv2.forward_stats(out, self.bn2), self.bn2, residual=identity, relu=True, counted=True)
+            res_join = None
+        return bn_act(self.conv2.forward_stats(out, self.bn2), self.bn2, residual=identity, relu=True, counted=True,
+                      res_join=res_join)
 
 
 class ResNet18(nn.Module):

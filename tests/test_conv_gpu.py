@@ -366,3 +366,45 @@ def test_conv_512(shape, direct, dtype):
     assert _rel(wg.grad, dwr) <= 2e-4
     if C >= 8:
         assert _rel(xg.grad, dxr) <= tol
+
+
+# ---------------------------------------------------------------------------- fused residual add
+# sqr_conv2d_bwd_data_acc: dx = bwd_data(dy) + addend.  Each dgrad that feeds a residual block's
+# input: layer-1 persistent kernel (N=4 and the bench batch: band / ring wrap, the ACC store
+# order), the tiled kernels of layers 2-4, the direct stride-2 kernel, and the implicit-GEMM +
+# add fallback (1x1 / fp32).  Reference: float64 dgrad of the same rounded operands + addend.
+ACC_SHAPES = [
+    (4, 64, 64, 64, 3, 1), (64, 64, 64, 64, 3, 1), (48, 64, 64, 64, 3, 1),
+    (4, 128, 32, 128, 3, 1), (4, 256, 16, 256, 3, 1), (4, 512, 8, 512, 3, 1),
+    (4, 64, 64, 128, 3, 2), (4, 128, 32, 256, 3, 2), (4, 256, 16, 512, 3, 2), (64, 64, 64, 128, 3, 2),
+    (4, 64, 64, 128, 1, 2), (2, 64, 128, 64, 3, 1), (2, 64, 128, 128, 3, 2),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=["bf16", "f16", "f32"])
+@pytest.mark.parametrize("shape", ACC_SHAPES, ids=lambda s: "N%dC%dH%dK%dR%ds%d" % s)
+def test_conv_bwd_data_acc(shape, dtype):
+    from sqr import conv as sc
+    N, C, H, K, R, st = shape
+    if dtype == torch.float32 and N > 8:
+        pytest.skip("fp32 runs the implicit GEMM + add; the small batch covers it")
+    pad = R // 2
+    g = torch.Generator().manual_seed(11 * N + C + K + R)
+    Ho = (H + 2 * pad - R) // st + 1
+    w = torch.randn(K, C, R, R, generator=g) / (C * R * R) ** 0.5
+    gy = torch.randn(N, K, Ho, Ho, generator=g).to(dtype).float()
+    add = torch.randn(N, C, H, H, generator=g).to(dtype).float()
+    d = sc._desc(N, C, H, H, K, R, R, st, pad, dtype)
+    _, crsk = sc.pack_weight(w.to(DEV), d, True)
+    gyg = gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    addg = add.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dx = sc.conv2d_bwd_data_acc(gyg, crsk, d, addg)
+    plain = sc.conv2d_bwd_data(gyg, crsk, d)
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.to(dtype).double(), gy.double(), stride=st, padding=pad)
+    ref = ref + add.double()
+    tol = {torch.bfloat16: 1.2e-2, torch.float16: 2e-3, torch.float32: 1e-5}[dtype]
+    assert _rel(dx, ref) <= tol
+    # the fused sum equals the separate sum up to one rounding of the 16-bit result
+    assert _rel(dx, plain.double() + addg.double()) <= (1.0 if dtype == torch.float32 else 2.0) * tol
+    assert torch.equal(addg.cpu().float(), add.to(dtype).float())  # the addend is not modified

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--replays", type=int, default=5)
+    ap.add_argument("--acc", action="store_true", help="dgrad with a residual addend (sqr_conv2d_bwd_data_acc)")
     a = ap.parse_args()
     from sqr import conv as sc
     from sqr._lib import LIB_PATH, check, lib
@@ -41,10 +42,13 @@ def main():
     d = sc._desc(N, C, H, H, K, 3, 3, a.stride, 1, dt)
     krsc, crsk = sc.pack_weight(w, d, True)
     clk = torch.empty(a.reps, 2, dtype=torch.int64, device=dev)
+    add = torch.randn(N, C, H, H, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
 
     def one():
         if a.phase == "fwd":
             sc.conv2d_fwd(x, krsc, d, stats=True)
+        elif a.phase == "dgrad" and a.acc:
+            sc.conv2d_bwd_data_acc(gy, crsk, d, add)
         elif a.phase == "dgrad":
             sc.conv2d_bwd_data(gy, crsk, d)
         else:
@@ -77,7 +81,8 @@ def main():
         spans += [float(t) / khz.value * 1e3 for t in (v[ok, 1] - v[ok, 0]).tolist()]
     us = float(np.median(spans)) if spans else float("nan")
     flops = 2.0 * N * Ho * Ho * K * C * 9
-    print(json.dumps({"shape": a.shape, "stride": a.stride, "phase": a.phase, "dtype": a.dtype, "us": us,
+    print(json.dumps({"shape": a.shape, "stride": a.stride, "phase": a.phase + ("+acc" if a.acc else ""),
+                      "dtype": a.dtype, "us": us,
                       "tflops": flops / us / 1e6 if spans else None, "n": len(spans),
                       "lib": os.path.basename(LIB_PATH), "env": {k: v for k, v in os.environ.items()
                                                                  if k.startswith("SQR_")}}))
