@@ -204,6 +204,31 @@ int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* x, long lon
                const float* save_mean, const float* save_invstd, void* dx, void* dres, float* dgamma,
                float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Two-branch BatchNorm: y = act(bn_a(a.x) + bn_b(b.x)) — torchvision BasicBlock with a downsample,
+ * relu(bn2(conv2(.)) + bn_ds(conv_ds(x))) (torch/models.py:181).  One apply pass reads both conv
+ * outputs (the downsample branch's normalised tensor is never written); the backward reduces both
+ * BatchNorms in one pass over (dy, mask, a.x, b.x) and writes both input gradients in one pass.
+ * Training takes the batch statistics from each conv's sqr_conv2d_fwd_stats partials. */
+typedef struct sqr_bn_operand {
+  const void* x;            /* [M][C] conv output (NHWC), the op's dtype */
+  const float* stats;       /* training: [stats_rows][2][C] partials; eval: unused */
+  int stats_rows;
+  const float* gamma;       /* nullable (affine=False) */
+  const float* beta;
+  float* running_mean;      /* nullable when not tracking (training) */
+  float* running_var;
+  float momentum, eps;
+  float* save_mean;         /* training: written by fwd, read by bwd */
+  float* save_invstd;
+} sqr_bn_operand;
+size_t sqr_bn_add_workspace_bytes(long long M, int C);
+int sqr_bn_add_fwd(const sqr_bn_operand* a, const sqr_bn_operand* b, long long M, int C, int dtype, int training,
+                   int relu, void* y, uint8_t* relu_mask, void* workspace, size_t workspace_bytes, void* stream);
+/* training backward: g = dy * [y > 0]; dx_a / dx_b, dgamma / dbeta of both BatchNorms */
+int sqr_bn_add_bwd(const sqr_bn_operand* a, const sqr_bn_operand* b, const void* dy, const uint8_t* relu_mask,
+                   long long M, int C, int dtype, void* dx_a, void* dx_b, float* dgamma_a, float* dbeta_a,
+                   float* dgamma_b, float* dbeta_b, void* workspace, size_t workspace_bytes, void* stream);
+
 /* resnet stem: y = maxpool3x3/s2/p1(relu(bn(x))), x [N][H][W][C] NHWC; argmax [N][Ho][Wo][C] uint8
  * = window tap (dh*3+dw) of the first maximum (torch's tie rule), written when training. */
 size_t sqr_stem_workspace_bytes(int N, int H, int W, int C);

@@ -163,15 +163,16 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
 // one block per channel: thread t sums partials t, t+256, ... (independent loads in flight), then a
 // fixed xor-tree wave reduction and a fixed-order sum of the 4 waves (deterministic).  Returns
 // true on thread 0 only.
-template <typename P>
-__device__ __forceinline__ bool sum_partials(const P* __restrict__ part, int nblk, int C, double* s, int* cout) {
+// (partials [k][NS][C]: statistic 0 and statistic SB of channel c)
+template <typename P, int NS = 2, int SB = 1>
+__device__ __forceinline__ bool sum_partials_c(const P* __restrict__ part, int nblk, int C, int c, double* s) {
   __shared__ double red[2][4];
-  const int c = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   double a = 0.0, b = 0.0;
 #pragma unroll 4
   for (int k = t; k < nblk; k += 256) {
-    a += (double)part[(size_t)k * 2 * C + c];
-    b += (double)part[(size_t)k * 2 * C + C + c];
+    a += (double)part[(size_t)k * NS * C + c];
+    b += (double)part[(size_t)k * NS * C + SB * C + c];
   }
   a = wave_sum_d(a);
   b = wave_sum_d(b);
@@ -183,8 +184,12 @@ __device__ __forceinline__ bool sum_partials(const P* __restrict__ part, int nbl
   if (t != 0) return false;
   s[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
   s[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-  *cout = c;
   return true;
+}
+template <typename P>
+__device__ __forceinline__ bool sum_partials(const P* __restrict__ part, int nblk, int C, double* s, int* cout) {
+  *cout = blockIdx.x;
+  return sum_partials_c<P>(part, nblk, C, blockIdx.x, s);
 }
 
 // forward finalize: coef[0][c] = scale, coef[1][c] = shift; save_mean/save_invstd; running stats
@@ -311,6 +316,205 @@ __global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy
     V8<T>::store(dx + i * 8, o);
     if (dres) V8<T>::store(dres + i * 8, g);
   }
+}
+
+// ---------------------------------------------------------------- two-branch BatchNorm
+// relu(bn_a(xa) + bn_b(xb)): torchvision BasicBlock with a downsample (out = bn2(conv2) +
+// bn_ds(conv_ds), then ReLU).  The downsample branch's normalised tensor is never written: one
+// apply pass reads both conv outputs; the backward reduces both BatchNorms' sums in one pass over
+// (dy, mask, xa, xb) (sum g is shared) and writes both input gradients in one pass.
+struct FinJob {
+  const float* part;  // forward: f32 partials [nblk][2][C]; backward: unused (shared f64 partials)
+  int nblk;
+  const float *gamma, *beta;
+  float *rmean, *rvar;
+  float momentum, eps;
+  float *save_mean, *save_invstd;
+  float* coef;  // forward: [scale C][shift C]; backward: [k1 C][k2 C][k3 C]
+  float *dgamma, *dbeta;
+};
+
+__device__ __forceinline__ void fwd_finalize_one(const FinJob& j, int c, int M, int C, double s, double ss) {
+  const double mean = s / M;
+  double var = ss / M - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const double invstd = 1.0 / sqrt(var + (double)j.eps);
+  const float g = j.gamma ? j.gamma[c] : 1.f, bt = j.beta ? j.beta[c] : 0.f;
+  j.coef[c] = (float)(g * invstd);
+  j.coef[C + c] = (float)(bt - mean * g * invstd);
+  j.save_mean[c] = (float)mean;
+  j.save_invstd[c] = (float)invstd;
+  if (j.rmean) {
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    j.rmean[c] = (float)((1.0 - j.momentum) * j.rmean[c] + j.momentum * mean);
+    j.rvar[c] = (float)((1.0 - j.momentum) * j.rvar[c] + j.momentum * unb);
+  }
+}
+
+// grid 2C: blocks [0, C) finalize BN a, [C, 2C) BN b (same arithmetic as fwd_finalize_kernel)
+__global__ void fwd_finalize2_kernel(FinJob a, FinJob b, int M, int C) {
+  const bool second = (int)blockIdx.x >= C;
+  const FinJob& j = second ? b : a;
+  const int c = second ? blockIdx.x - C : blockIdx.x;
+  double acc[2];
+  if (!sum_partials_c<float>(j.part, j.nblk, C, c, acc)) return;
+  fwd_finalize_one(j, c, M, C, acc[0], acc[1]);
+}
+
+// y = act(xa*sa + ta + xb*sb + tb)
+template <typename T>
+__global__ void __launch_bounds__(256) apply2_kernel(const T* __restrict__ xa, const T* __restrict__ xb,
+                                                     const float* __restrict__ coef_a,
+                                                     const float* __restrict__ coef_b, int C, int nvec, int relu,
+                                                     T* __restrict__ y, uint8_t* __restrict__ mask) {
+  const int lv = __builtin_ctz(C >> 3);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nvec) return;
+  const int v = i & ((1 << lv) - 1);
+  float va[8], vb[8], sa[8], ta[8], sb[8], tb[8];
+  V8<T>::load(xa + i * 8, va);
+  V8<T>::load(xb + i * 8, vb);
+  load8f(coef_a + v * 8, sa);
+  load8f(coef_a + C + v * 8, ta);
+  load8f(coef_b + v * 8, sb);
+  load8f(coef_b + C + v * 8, tb);
+  float o[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    o[k] = fmaf(va[k], sa[k], ta[k]) + fmaf(vb[k], sb[k], tb[k]);
+    if (relu) o[k] = fmaxf(o[k], 0.f);
+  }
+  V8<T>::store(y + i * 8, o);
+  if (mask) {
+    uint32_t mb = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mb |= (uint32_t)((float)(T)o[k] > 0.f) << k;
+    mask[i] = (uint8_t)mb;
+  }
+}
+
+// per-block f64 partials [blk][3][C]: sum g, sum g*(xa - mean_a), sum g*(xb - mean_b), g = dy*[mask]
+template <typename T>
+__global__ void __launch_bounds__(256) reduce2_kernel(const T* __restrict__ xa, const T* __restrict__ xb,
+                                                      const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                      const float* __restrict__ mean_a,
+                                                      const float* __restrict__ mean_b, int M, int C, int chunk,
+                                                      double* __restrict__ part) {
+  extern __shared__ double red[];  // [rows][V][24]
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x;
+  const int row = tid / V, v = tid - row * V;
+  double s0[8], s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0[i] = s1[i] = s2[i] = 0.0;
+  float mua[8], mub[8];
+  load8f(mean_a + v * 8, mua);
+  load8f(mean_b + v * 8, mub);
+  const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
+  constexpr int U = 4;
+  for (int pb = p0 + row; pb < p1; pb += U * rows) {
+    float a[U][8], b[U][8], g[U][8];
+    uint32_t mbits[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = min(pb + u * rows, p1 - 1);
+      const size_t off = (size_t)p * C + v * 8;
+      V8<T>::load(xa + off, a[u]);
+      V8<T>::load(xb + off, b[u]);
+      V8<T>::load(dy + off, g[u]);
+      mbits[u] = mask ? (uint32_t)mask[off >> 3] : 0xffu;
+    }
+    float f0[8], f1[8], f2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0[i] = f1[i] = f2[i] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t mb = pb + u * rows < p1 ? mbits[u] : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float gg = (mb >> i) & 1 ? g[u][i] : 0.f;
+        f0[i] += gg;
+        f1[i] = fmaf(gg, a[u][i] - mua[i], f1[i]);
+        f2[i] = fmaf(gg, b[u][i] - mub[i], f2[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s0[i] += (double)f0[i];
+      s1[i] += (double)f1[i];
+      s2[i] += (double)f2[i];
+    }
+  }
+  double* dst = red + ((size_t)row * V + v) * 24;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dst[i] = s0[i];
+    dst[8 + i] = s1[i];
+    dst[16 + i] = s2[i];
+  }
+  __syncthreads();
+  double* out = part + (size_t)blockIdx.x * 3 * C;
+  for (int t = tid; t < V * 24; t += 256) {
+    const int vv = t / 24, i = t - vv * 24;
+    double acc = 0.0;
+    for (int r = 0; r < rows; ++r) acc += red[((size_t)r * V + vv) * 24 + i];
+    out[(i >> 3) * C + vv * 8 + (i & 7)] = acc;
+  }
+}
+
+// grid 2C: BN a from (sum g, sum g*(xa-mean_a)), BN b from (sum g, sum g*(xb-mean_b))
+__global__ void bwd_finalize2_kernel(const double* __restrict__ part, int nblk, int M, int C, FinJob a, FinJob b) {
+  const bool second = (int)blockIdx.x >= C;
+  const FinJob& j = second ? b : a;
+  const int c = second ? blockIdx.x - C : blockIdx.x;
+  double acc[2];
+  const bool mine = second ? sum_partials_c<double, 3, 2>(part, nblk, C, c, acc)
+                           : sum_partials_c<double, 3, 1>(part, nblk, C, c, acc);
+  if (!mine) return;
+  const double sg = acc[0], sgx = acc[1];
+  const double is = j.save_invstd[c], mu = j.save_mean[c];
+  const double dgam = sgx * is;
+  if (j.dgamma) j.dgamma[c] = (float)dgam;
+  if (j.dbeta) j.dbeta[c] = (float)sg;
+  const double ak = (j.gamma ? j.gamma[c] : 1.0) * is;
+  const double k3 = -ak * is * dgam / M;
+  j.coef[c] = (float)ak;
+  j.coef[2 * C + c] = (float)k3;
+  j.coef[C + c] = (float)(-ak * sg / M - k3 * mu);
+}
+
+// dx_a = k1a*g + k3a*xa + k2a,  dx_b = k1b*g + k3b*xb + k2b,  g = dy*[mask]
+template <typename T>
+__global__ void __launch_bounds__(256) bwd_apply2_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                         const T* __restrict__ xa, const T* __restrict__ xb,
+                                                         const float* __restrict__ ca, const float* __restrict__ cb,
+                                                         int C, int nvec, T* __restrict__ dxa, T* __restrict__ dxb) {
+  const int lv = __builtin_ctz(C >> 3);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nvec) return;
+  const int v = i & ((1 << lv) - 1);
+  float g[8], a[8], b[8], k[6][8];
+  V8<T>::load(dy + i * 8, g);
+  if (mask) {
+    const uint32_t mb = mask[i];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (mb >> e) & 1 ? g[e] : 0.f;
+  }
+  V8<T>::load(xa + i * 8, a);
+  V8<T>::load(xb + i * 8, b);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    load8f(ca + q * C + v * 8, k[q]);
+    load8f(cb + q * C + v * 8, k[3 + q]);
+  }
+  float oa[8], ob[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    oa[e] = fmaf(k[0][e], g[e], fmaf(k[2][e], a[e], k[1][e]));
+    ob[e] = fmaf(k[3][e], g[e], fmaf(k[5][e], b[e], k[4][e]));
+  }
+  V8<T>::store(dxa + i * 8, oa);
+  V8<T>::store(dxb + i * 8, ob);
 }
 
 // ---------------------------------------------------------------- stem: BN + ReLU + MaxPool(3,2,1)
@@ -841,4 +1045,133 @@ extern "C" int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int
                                save_mean, save_invstd, workspace, st, stats, stats_rows);
   return stem_fwd_impl<float>(x, N, H, W, C, gamma, beta, running_mean, running_var, momentum, eps, 1, y, argmax,
                               save_mean, save_invstd, workspace, st, stats, stats_rows);
+}
+
+// ---------------------------------------------------------------- two-branch BatchNorm (host)
+namespace {
+FinJob fin_job(const sqr_bn_operand* o, float* coef) {
+  FinJob j;
+  j.part = o->stats;
+  j.nblk = o->stats_rows;
+  j.gamma = o->gamma;
+  j.beta = o->beta;
+  j.rmean = o->running_mean;
+  j.rvar = o->running_var;
+  j.momentum = o->momentum;
+  j.eps = o->eps;
+  j.save_mean = o->save_mean;
+  j.save_invstd = o->save_invstd;
+  j.coef = coef;
+  j.dgamma = j.dbeta = nullptr;
+  return j;
+}
+
+int check_pair(const sqr_bn_operand* a, const sqr_bn_operand* b, long long M, int C, int dtype) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(a && b && a->x && b->x, "bn_add: null operand");
+  return 0;
+}
+}  // namespace
+
+extern "C" size_t sqr_bn_add_workspace_bytes(long long M, int C) {
+  if (M < 1 || C < 8) return 0;
+  const RedPlan p = red_plan((int)M, C);
+  return a256((size_t)p.nblk * 3 * C * sizeof(double)) + a256((size_t)6 * C * sizeof(float));
+}
+
+template <typename T>
+static int bn_add_fwd_impl(const sqr_bn_operand* a, const sqr_bn_operand* b, int M, int C, int training, int relu,
+                           void* y, uint8_t* mask, void* ws, hipStream_t st) {
+  const RedPlan p = red_plan(M, C);
+  float* ca = (float*)((char*)ws + a256((size_t)p.nblk * 3 * C * sizeof(double)));
+  float* cb = ca + 3 * C;
+  if (training) {
+    hipLaunchKernelGGL(fwd_finalize2_kernel, dim3(2 * C), dim3(256), 0, st, fin_job(a, ca), fin_job(b, cb), M, C);
+    SQR_HIP_LAUNCH_CHECK("bn fwd_finalize2_kernel");
+  } else {
+    int rc = bn_infer_coef(C, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ca, st);
+    if (!rc) rc = bn_infer_coef(C, b->gamma, b->beta, b->running_mean, b->running_var, b->eps, cb, st);
+    if (rc) return rc;
+  }
+  const int nvec = M * (C / 8);
+  hipLaunchKernelGGL((apply2_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)a->x, (const T*)b->x, ca,
+                     cb, C, nvec, relu, (T*)y, relu ? mask : nullptr);
+  SQR_HIP_LAUNCH_CHECK("bn apply2_kernel");
+  return 0;
+}
+
+extern "C" int sqr_bn_add_fwd(const sqr_bn_operand* a, const sqr_bn_operand* b, long long M, int C, int dtype,
+                              int training, int relu, void* y, uint8_t* relu_mask, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  int rc = check_pair(a, b, M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(y && workspace, "bn_add_fwd: null pointer");
+  if (training) {
+    SQR_CHECK_ARG(a->stats && a->stats_rows > 0 && b->stats && b->stats_rows > 0,
+                  "bn_add_fwd: training needs the convs' statistics partials");
+    SQR_CHECK_ARG(a->save_mean && a->save_invstd && b->save_mean && b->save_invstd,
+                  "bn_add_fwd: training needs save_mean/save_invstd");
+  } else {
+    SQR_CHECK_ARG(a->running_mean && a->running_var && b->running_mean && b->running_var,
+                  "bn_add_fwd: eval needs running statistics");
+  }
+  if (workspace_bytes < sqr_bn_add_workspace_bytes(M, C)) {
+    set_error("bn_add_fwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16) return bn_add_fwd_impl<bf16>(a, b, (int)M, C, training, relu, y, relu_mask, workspace, st);
+  if (dtype == SQR_DTYPE_F16) return bn_add_fwd_impl<f16>(a, b, (int)M, C, training, relu, y, relu_mask, workspace, st);
+  return bn_add_fwd_impl<float>(a, b, (int)M, C, training, relu, y, relu_mask, workspace, st);
+}
+
+template <typename T>
+static int bn_add_bwd_impl(const sqr_bn_operand* a, const sqr_bn_operand* b, const void* dy, const uint8_t* mask,
+                           int M, int C, void* dxa, void* dxb, float* dga, float* dba, float* dgb, float* dbb,
+                           void* ws, hipStream_t st) {
+  const RedPlan p = red_plan(M, C);
+  double* part = (double*)ws;
+  float* ca = (float*)((char*)ws + a256((size_t)p.nblk * 3 * C * sizeof(double)));
+  float* cb = ca + 3 * C;
+  const size_t lds = (size_t)p.rows * (C / 8) * 24 * sizeof(double);
+  hipLaunchKernelGGL((reduce2_kernel<T>), dim3(p.nblk), dim3(256), lds, st, (const T*)a->x, (const T*)b->x,
+                     (const T*)dy, mask, a->save_mean, b->save_mean, M, C, p.chunk, part);
+  SQR_HIP_LAUNCH_CHECK("bn reduce2_kernel");
+  FinJob ja = fin_job(a, ca), jb = fin_job(b, cb);
+  ja.dgamma = dga;
+  ja.dbeta = dba;
+  jb.dgamma = dgb;
+  jb.dbeta = dbb;
+  hipLaunchKernelGGL(bwd_finalize2_kernel, dim3(2 * C), dim3(256), 0, st, part, p.nblk, M, C, ja, jb);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_finalize2_kernel");
+  const int nvec = M * (C / 8);
+  hipLaunchKernelGGL((bwd_apply2_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dy, mask,
+                     (const T*)a->x, (const T*)b->x, ca, cb, C, nvec, (T*)dxa, (T*)dxb);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_apply2_kernel");
+  return 0;
+}
+
+extern "C" int sqr_bn_add_bwd(const sqr_bn_operand* a, const sqr_bn_operand* b, const void* dy,
+                              const uint8_t* relu_mask, long long M, int C, int dtype, void* dx_a, void* dx_b,
+                              float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  int rc = check_pair(a, b, M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(dy && dx_a && dx_b && workspace, "bn_add_bwd: null pointer");
+  SQR_CHECK_ARG(a->save_mean && a->save_invstd && b->save_mean && b->save_invstd,
+                "bn_add_bwd: needs the forward's save_mean/save_invstd");
+  if (workspace_bytes < sqr_bn_add_workspace_bytes(M, C)) {
+    set_error("bn_add_bwd: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return bn_add_bwd_impl<bf16>(a, b, dy, relu_mask, (int)M, C, dx_a, dx_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b,
+                                 workspace, st);
+  if (dtype == SQR_DTYPE_F16)
+    return bn_add_bwd_impl<f16>(a, b, dy, relu_mask, (int)M, C, dx_a, dx_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b,
+                                workspace, st);
+  return bn_add_bwd_impl<float>(a, b, dy, relu_mask, (int)M, C, dx_a, dx_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b,
+                                workspace, st);
 }

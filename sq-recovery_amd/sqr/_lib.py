@@ -28,6 +28,12 @@ class SqrPackJob(ctypes.Structure):
     _fields_ = [("w_kcrs", c_void_p), ("desc", SqrConvDesc), ("w_krsc", c_void_p), ("w_crsk", c_void_p)]
 
 
+class SqrBnOperand(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("stats", c_void_p), ("stats_rows", c_int), ("gamma", c_void_p), ("beta", c_void_p),
+                ("running_mean", c_void_p), ("running_var", c_void_p), ("momentum", c_float), ("eps", c_float),
+                ("save_mean", c_void_p), ("save_invstd", c_void_p)]
+
+
 class SqrTailDesc(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("B", "P", "C0", "F1", "F2", "dtype")] + \
         [("w0", c_void_p), ("b0", c_void_p), ("w1", c_void_p), ("b1", c_void_p),
@@ -81,6 +87,12 @@ SIGNATURES = {
     "sqr_conv2d_bwd_weight_col": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                           c_size_t, c_void_p]),
     "sqr_bn_workspace_bytes": (c_size_t, [ctypes.c_longlong, c_int]),
+    "sqr_bn_add_workspace_bytes": (c_size_t, [ctypes.c_longlong, c_int]),
+    "sqr_bn_add_fwd": (c_int, [ctypes.POINTER(SqrBnOperand), ctypes.POINTER(SqrBnOperand), ctypes.c_longlong, c_int,
+                               c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_bn_add_bwd": (c_int, [ctypes.POINTER(SqrBnOperand), ctypes.POINTER(SqrBnOperand), c_void_p, c_void_p,
+                               ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_bn_fwd": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_float, c_float, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_size_t, c_void_p]),

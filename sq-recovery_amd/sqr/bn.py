@@ -11,7 +11,7 @@ import ctypes
 import torch
 
 from . import gradbuf
-from ._lib import check, lib, ptr, stream_ptr
+from ._lib import SqrBnOperand, check, lib, ptr, stream_ptr
 
 _CL = torch.channels_last
 
@@ -141,6 +141,112 @@ def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None):
     rv = bn.running_var if bn.track_running_stats else None
     return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
                          _check_stats(stats, x), res_join if residual is not None else None)
+
+
+def _operand(x, stats, weight, bias, rmean, rvar, momentum, eps, mean, invstd):
+    o = SqrBnOperand()
+    o.x = x.data_ptr()
+    o.stats = stats.data_ptr() if stats is not None else None
+    o.stats_rows = stats.shape[0] if stats is not None else 0
+    o.gamma = weight.data_ptr() if weight is not None else None
+    o.beta = bias.data_ptr() if bias is not None else None
+    o.running_mean = rmean.data_ptr() if rmean is not None else None
+    o.running_var = rvar.data_ptr() if rvar is not None else None
+    o.momentum, o.eps = momentum, eps
+    o.save_mean, o.save_invstd = mean.data_ptr(), invstd.data_ptr()
+    return o
+
+
+class BNAddActFn(torch.autograd.Function):
+    """relu?(bn_a(xa) + bn_b(xb)) — a BasicBlock's bn2(conv2) + downsample bn_ds(conv_ds) + ReLU as
+    one op (libsqr sqr_bn_add_*): the downsample branch is never normalised into its own tensor, and
+    its BatchNorm backward shares the block output's gradient pass."""
+
+    @staticmethod
+    def forward(ctx, xa, wa, ba, rma, rva, xb, wb, bb, rmb, rvb, relu, training, mom_a, mom_b, eps_a, eps_b,
+                stats_a, stats_b):
+        xa = xa.contiguous(memory_format=_CL)
+        xb = xb.to(xa.dtype).contiguous(memory_format=_CL)
+        N, C, H, W = xa.shape
+        M = N * H * W
+        y = torch.empty_like(xa, memory_format=_CL)
+        f32 = dict(dtype=torch.float32, device=xa.device)
+        ma, ia, mb, ib = (torch.empty(C, **f32) for _ in range(4))
+        mask = torch.empty(M * C // 8, dtype=torch.uint8, device=xa.device) if (relu and training) else None
+        oa = _operand(xa, stats_a, wa, ba, rma, rva, mom_a, eps_a, ma, ia)
+        ob = _operand(xb, stats_b, wb, bb, rmb, rvb, mom_b, eps_b, mb, ib)
+        L = lib()
+        n = L.sqr_bn_add_workspace_bytes(ctypes.c_longlong(M), C)
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=xa.device)
+        check(L.sqr_bn_add_fwd(ctypes.byref(oa), ctypes.byref(ob), ctypes.c_longlong(M), C, _dt(xa), int(training),
+                               int(relu), ptr(y), ptr(mask), ptr(ws), n, stream_ptr(xa.device)), "sqr_bn_add_fwd")
+        ctx.training = training
+        ctx.eps = (eps_a, eps_b)
+        ctx.pids = (id(wa), id(ba), id(wb), id(bb))
+        if training:
+            ctx.save_for_backward(xa, xb, mask, wa, wb, ma, ia, mb, ib)
+        else:
+            ctx.save_for_backward(xa, xb, y if relu else None, wa, wb, rma.clone(), rva.clone(), rmb.clone(),
+                                  rvb.clone())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xa, xb, ym, wa, wb, ma, va, mb, vb = ctx.saved_tensors
+        dy = dy.to(xa.dtype).contiguous(memory_format=_CL)
+        N, C, H, W = xa.shape
+        M = N * H * W
+        if not ctx.training:  # eval-mode backward (constant statistics): plain torch
+            g = dy.float() * (ym > 0) if ym is not None else dy.float()
+            out = []
+            for x, w, m, v, eps in ((xa, wa, ma, va, ctx.eps[0]), (xb, wb, mb, vb, ctx.eps[1])):
+                invstd = torch.rsqrt(v + eps)
+                xhat = (x.float() - m.view(1, C, 1, 1)) * invstd.view(1, C, 1, 1)
+                out.append(((g * (w * invstd).view(1, C, 1, 1)).to(x.dtype), (g * xhat).sum((0, 2, 3)),
+                            g.sum((0, 2, 3))))
+            (dxa, dga, dba), (dxb, dgb, dbb) = out
+            return dxa, dga, dba, None, None, dxb, dgb, dbb, None, None, None, None, None, None, None, None, None, None
+        dxa = torch.empty_like(xa, memory_format=_CL)
+        dxb = torch.empty_like(xb, memory_format=_CL)
+        dga = gradbuf.out(ctx.pids[0], (C,), xa.device)
+        dba = gradbuf.out(ctx.pids[1], (C,), xa.device)
+        dgb = gradbuf.out(ctx.pids[2], (C,), xa.device)
+        dbb = gradbuf.out(ctx.pids[3], (C,), xa.device)
+        oa = _operand(xa, None, wa, None, None, None, 0.0, ctx.eps[0], ma, va)
+        ob = _operand(xb, None, wb, None, None, None, 0.0, ctx.eps[1], mb, vb)
+        L = lib()
+        n = L.sqr_bn_add_workspace_bytes(ctypes.c_longlong(M), C)
+        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=xa.device)
+        check(L.sqr_bn_add_bwd(ctypes.byref(oa), ctypes.byref(ob), ptr(dy), ptr(ym), ctypes.c_longlong(M), C, _dt(xa),
+                               ptr(dxa), ptr(dxb), ptr(dga), ptr(dba), ptr(dgb), ptr(dbb), ptr(ws), n,
+                               stream_ptr(xa.device)), "sqr_bn_add_bwd")
+        gradbuf.written(ctx.pids)
+        return dxa, dga, dba, None, None, dxb, dgb, dbb, None, None, None, None, None, None, None, None, None, None
+
+
+def bn_add_act(xa, bn_a, xb, bn_b, relu=True, counted=False):
+    """relu?(bn_a(xa) + bn_b(xb)) (two nn.BatchNorm2d, same channel count).  xa / xb may be
+    (y, partials) pairs from stats-producing convs; training mode needs both partials."""
+    xa, sa = _split(xa)
+    xb, sb = _split(xb)
+    ta = bn_a.training or not bn_a.track_running_stats
+    tb = bn_b.training or not bn_b.track_running_stats
+    if ta != tb:
+        raise ValueError("sqr bn_add_act: both BatchNorms must be in the same mode")
+    if ta and (sa is None or sb is None):
+        raise ValueError("sqr bn_add_act: training needs both convs' statistics partials")
+    for bn in (bn_a, bn_b):
+        if ta and bn.track_running_stats and not counted:
+            bn.num_batches_tracked.add_(1)
+    args = []
+    for bn in (bn_a, bn_b):
+        mom = _momentum(bn) if (ta and bn.track_running_stats) else 0.0
+        args.append((bn.running_mean if bn.track_running_stats else None,
+                     bn.running_var if bn.track_running_stats else None, mom, float(bn.eps)))
+    (rma, rva, moma, epsa), (rmb, rvb, momb, epsb) = args
+    return BNAddActFn.apply(xa, bn_a.weight, bn_a.bias, rma, rva, xb, bn_b.weight, bn_b.bias, rmb, rvb, bool(relu),
+                            bool(ta), moma, momb, epsa, epsb, _check_stats(sa, xa) if ta else None,
+                            _check_stats(sb, xb) if ta else None)
 
 
 class StemFn(torch.autograd.Function):

@@ -159,3 +159,63 @@ def test_stem_stats_fused(dtype):
         b = stem(y, bn_b)
     assert _rel(a, b) <= (1e-5 if dtype == torch.float32 else 1e-2)
     assert _rel(bn_a.running_var, bn_b.running_var) <= 1e-5
+
+
+def _partials(x, rows=3):
+    """[rows][2][C] f32 (sum, sum of squares) over disjoint pixel sets — what a stats-producing conv
+    epilogue hands the BatchNorm."""
+    N, C, H, W = x.shape
+    flat = x.detach().float().permute(0, 2, 3, 1).reshape(-1, C)
+    parts = [torch.stack([p.sum(0), (p * p).sum(0)]) for p in flat.chunk(rows)]
+    return torch.stack(parts).contiguous()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
+@pytest.mark.parametrize("cfg", [(4, 128, 16, True), (2, 256, 8, True), (3, 512, 4, True), (2, 64, 9, False),
+                                 (64, 128, 32, True)],
+                         ids=lambda c: "N%dC%dH%d_relu%d" % c)
+@pytest.mark.parametrize("training", [True, False], ids=["train", "eval"])
+def test_bn_add_act(cfg, dtype, training):
+    """relu(bn_a(xa) + bn_b(xb)) — BasicBlock bn2(conv2) + downsample bn_ds(conv_ds) as one op
+    (sqr_bn_add_fwd/_bwd) — vs two float64 nn.BatchNorm2d on the CPU: output, both input
+    gradients, all four parameter gradients, both running statistics."""
+    from sqr.bn import bn_add_act
+    N, C, H, relu = cfg
+    g = torch.Generator().manual_seed(C + H + 7)
+    xa = torch.randn(N, C, H, H, generator=g) * 2 + 0.5
+    xb = torch.randn(N, C, H, H, generator=g) * 0.7 - 0.3
+    gy = torch.randn(N, C, H, H, generator=g)
+    if dtype != torch.float32:
+        xa, xb, gy = xa.to(dtype).float(), xb.to(dtype).float(), gy.to(dtype).float()
+    ra, rb = _bn(C, 1).double().train(training), _bn(C, 2).double().train(training)
+    ga = copy.deepcopy(_bn(C, 1)).to(DEV).train(training)
+    gb = copy.deepcopy(_bn(C, 2)).to(DEV).train(training)
+    xar, xbr = xa.double().requires_grad_(True), xb.double().requires_grad_(True)
+    pre = ra(xar) + rb(xbr)
+    y_ref = F.relu(pre) if relu else pre
+    y_ref.backward(gy.double())
+    # elements whose pre-activation is within f32 rounding of 0 (|pre| ~1e-8: the kernel's f32 sum may
+    # land on either side, and fp16 stores it as 0) have an ambiguous ReLU mask: their own input
+    # gradient is left out of the comparison (their effect on the batch sums is negligible)
+    sure = (pre.detach().abs() > 1e-5) if relu else torch.ones_like(pre, dtype=torch.bool)
+
+    cl = dict(memory_format=torch.channels_last)
+    xag = xa.to(DEV).to(dtype).contiguous(**cl).requires_grad_(True)
+    xbg = xb.to(DEV).to(dtype).contiguous(**cl).requires_grad_(True)
+    a_in = (xag, _partials(xa).to(DEV)) if training else xag
+    b_in = (xbg, _partials(xb, 5).to(DEV)) if training else xbg
+    y = bn_add_act(a_in, ga, b_in, gb, relu=relu)
+    assert y.dtype == dtype and y.is_contiguous(**cl)
+    y.backward(gy.to(DEV).to(dtype).contiguous(**cl))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    gtol = tol if dtype == torch.float32 else 3e-2
+    assert _rel(y, y_ref) <= tol
+    assert int((~sure).sum()) <= 1e-5 * sure.numel() + 4
+    assert _rel(xag.grad.cpu().double() * sure, xar.grad * sure) <= gtol
+    assert _rel(xbg.grad.cpu().double() * sure, xbr.grad * sure) <= gtol
+    for m, r in ((ga, ra), (gb, rb)):
+        assert _rel(m.weight.grad, r.weight.grad) <= gtol
+        assert _rel(m.bias.grad, r.bias.grad) <= gtol
+        assert _rel(m.running_mean, r.running_mean) <= 1e-6
+        assert _rel(m.running_var, r.running_var) <= 1e-6
+        assert int(m.num_batches_tracked) == int(r.num_batches_tracked)

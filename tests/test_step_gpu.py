@@ -26,9 +26,13 @@ def _round16(dt):
 
 
 def _emulated(ref, dt):
-    """ref_torch model (float32) whose activations are rounded to dt where the GPU step stores them."""
+    """ref_torch model (float32) whose activations are rounded to dt where the GPU step stores them.
+    The downsample BatchNorm's output is not stored by the GPU step (sqr_bn_add_fwd adds it to bn2's
+    in f32 before the one rounding), so it is not rounded here either."""
     hooks = []
-    for m in ref.modules():
+    for name, m in ref.named_modules():
+        if isinstance(m, nn.BatchNorm2d) and name.endswith("downsample.1"):
+            continue
         if isinstance(m, (nn.Conv2d, nn.BatchNorm2d, nn.MaxPool2d, nn.ReLU)):
             hooks.append(m.register_forward_hook(_round16(dt)))
     return hooks
@@ -87,9 +91,10 @@ def test_bench_step_gradients_vs_f64(config, batch):
         e_gpu = _rel_err(g_gpu[n], b)
         e_emu = _rel_err(g_emu[n], b)
         worst.append((e_gpu / max(e_emu, 1e-4), n, e_gpu, e_emu))
-        assert e_gpu <= 3 * e_emu + 1e-3, (n, e_gpu, e_emu)
     worst.sort(reverse=True)
-    print("worst gpu/emulated error ratios:", ["%s %.2e/%.2e" % (n, a, b) for _, n, a, b in worst[:5]])
+    print("worst gpu/emulated error ratios:", ["%s %.2e/%.2e" % (n, a, b) for _, n, a, b in worst[:8]])
+    for _, n, e_gpu, e_emu in worst:
+        assert e_gpu <= 3 * e_emu + 1e-3, (n, e_gpu, e_emu)
     # the step then applied Adam: every parameter moved, by at most ~lr (Adam's first-order bound)
     for n, p in tr.net.named_parameters():
         delta = (p.detach().cpu() - sd[n]).abs().max().item()
