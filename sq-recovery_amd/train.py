@@ -37,6 +37,7 @@ from classes import ExplicitLoss, H5Dataset, ImplicitLoss, IoUAccuracy, Syntheti
 from helpers import load_model, parse_csv, save_compare_images, save_model  # noqa: E402
 from models import ResNetSQ  # noqa: E402
 from sqr import amp, dist  # noqa: E402
+from sqr.data import DevicePrefetcher  # noqa: E402
 from sqr.optim import Adam  # noqa: E402
 
 
@@ -66,7 +67,7 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def _batches(dataset, rank, world, batch_size):
+def _batches(dataset, rank, world, batch_size, device=torch.device("cpu")):
     """This rank's batches of the current split (contiguous shard, no shuffle, like the reference;
     the last batch may be partial, as with the reference's DataLoader)."""
     idx = dist.shard(len(dataset), rank, world)
@@ -76,8 +77,10 @@ def _batches(dataset, rank, world, batch_size):
             j = min(i + batch_size, idx.stop)
             yield (dataset.images[off + i:off + j], dataset.labels[off + i:off + j])
         return
-    loader = data.DataLoader(data.Subset(dataset, list(idx)), batch_size=batch_size, shuffle=False, num_workers=4)
-    yield from loader
+    # pinned-memory workers + side-stream prefetch of the next batch (sqr.data.DevicePrefetcher)
+    loader = data.DataLoader(data.Subset(dataset, list(idx)), batch_size=batch_size, shuffle=False, num_workers=4,
+                             pin_memory=device.type == "cuda")
+    yield from DevicePrefetcher(loader, device)
 
 
 def main(argv=None):
@@ -136,7 +139,7 @@ def main(argv=None):
         net.train()
         dataset.set_mode(0)
         n_items = len(dataset)
-        for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size)):
+        for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size, device)):
             if args.max_steps and batch_idx >= args.max_steps:
                 break
             x, true_labels = x.to(device, non_blocking=True), true_labels.to(device, non_blocking=True)
@@ -169,7 +172,7 @@ def main(argv=None):
         net.eval()
         dataset.set_mode(1)
         with torch.no_grad():
-            for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size)):
+            for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size, device)):
                 if args.max_steps and batch_idx >= args.max_steps:
                     break
                 x, true_labels = x.to(device), true_labels.to(device)
