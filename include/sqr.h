@@ -170,6 +170,16 @@ int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_
  * their epilogues (the sum is never a separate pass); other shapes add after the GEMM. */
 int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void* dx, const void* addend,
                             const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
+/* Backward-data of a conv whose input is a BatchNorm+ReLU output — a BasicBlock's conv2 into bn1
+ * (torch/models.py:181): g_out = bwd_data(dy) * relu_mask (the BatchNorm's ReLU mask, 1 bit per
+ * element) and stats receives that BatchNorm's backward sums (sum g, sum g*(bn_x - bn_mean)) as
+ * f32 partial rows [*stats_rows][2][C] — computed in the direct kernels' epilogues, so
+ * sqr_bn_bwd_stats needs no reduction pass over (g, x).  stats must hold
+ * sqr_conv2d_bwd_data_bn_stats_floats(d) floats. */
+size_t sqr_conv2d_bwd_data_bn_stats_floats(const sqr_conv_desc* d);
+int sqr_conv2d_bwd_data_bn(const void* dy, const void* w_crsk, void* g_out, const void* bn_x,
+                           const uint8_t* relu_mask, const float* bn_mean, float* stats, int* stats_rows,
+                           const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
 /* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
 int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                           void* workspace, size_t workspace_bytes, void* stream);
@@ -203,6 +213,11 @@ int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, const float* 
 int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* x, long long M, int C, int dtype, const float* gamma,
                const float* save_mean, const float* save_invstd, void* dx, void* dres, float* dgamma,
                float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
+/* sqr_bn_bwd from sqr_conv2d_bwd_data_bn's partials: g already masked; dx = k1*g + k3*x + k2,
+ * dgamma, dbeta.  workspace >= 3*C floats. */
+int sqr_bn_bwd_stats(const void* g, const void* x, long long M, int C, int dtype, const float* stats, int stats_rows,
+                     const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
+                     float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Two-branch BatchNorm: y = act(bn_a(a.x) + bn_b(b.x)) — torchvision BasicBlock with a downsample,
  * relu(bn2(conv2(.)) + bn_ds(conv_ds(x))) (torch/models.py:181).  One apply pass reads both conv

@@ -268,8 +268,10 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
   }
 }
 
-// backward finalize: dgamma, dbeta and dx = k1*g + k3*x + k2 coefficients (coef[0..2][C])
-__global__ void bwd_finalize_kernel(const double* __restrict__ part, int nblk, int M, int C,
+// backward finalize: dgamma, dbeta and dx = k1*g + k3*x + k2 coefficients (coef[0..2][C]); partials
+// f64 from reduce_kernel or f32 from a backward-data epilogue (sqr_conv2d_bwd_data_bn)
+template <typename P>
+__global__ void bwd_finalize_kernel(const P* __restrict__ part, int nblk, int M, int C,
                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, float* __restrict__ dgamma,
                                     float* __restrict__ dbeta, float* __restrict__ coef) {
@@ -315,6 +317,53 @@ __global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy
     for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k3[k], xv[k], k2[k]));
     V8<T>::store(dx + i * 8, o);
     if (dres) V8<T>::store(dres + i * 8, g);
+  }
+}
+
+// g *= [relu mask] in place and f32 partials [blk][2][C] of (sum g, sum g*(x - mean)): the
+// implicit-GEMM fallback of sqr_conv2d_bwd_data_bn (the direct kernels do this in their epilogues)
+template <typename T>
+__global__ void __launch_bounds__(256) mask_reduce_kernel(T* __restrict__ g, const T* __restrict__ x,
+                                                          const uint8_t* __restrict__ mask,
+                                                          const float* __restrict__ mean, int M, int C, int chunk,
+                                                          float* __restrict__ part) {
+  extern __shared__ double red[];  // [rows][V][16]
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x;
+  const int row = tid / V, v = tid - row * V;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.0;
+  float mu[8];
+  load8f(mean + v * 8, mu);
+  const int p0 = blockIdx.x * chunk, p1 = min(p0 + chunk, M);
+  for (int p = p0 + row; p < p1; p += rows) {
+    const size_t off = (size_t)p * C + v * 8;
+    float gv[8], xv[8];
+    V8<T>::load(g + off, gv);
+    V8<T>::load(x + off, xv);
+    const uint32_t mb = mask ? (uint32_t)mask[off >> 3] : 0xffu;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      gv[i] = (mb >> i) & 1 ? gv[i] : 0.f;
+      sa[i] += (double)gv[i];
+      sb[i] += (double)gv[i] * (double)(xv[i] - mu[i]);
+    }
+    V8<T>::store(g + off, gv);
+  }
+  double* dst = red + ((size_t)row * V + v) * 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dst[i] = sa[i];
+    dst[8 + i] = sb[i];
+  }
+  __syncthreads();
+  float* out = part + (size_t)blockIdx.x * 2 * C;
+  for (int t = tid; t < V * 16; t += 256) {
+    const int vv = t >> 4, i = t & 15;
+    double acc = 0.0;
+    for (int r = 0; r < rows; ++r) acc += red[((size_t)r * V + vv) * 16 + i];
+    out[(i >> 3) * C + vv * 8 + (i & 7)] = (float)acc;
   }
 }
 
@@ -856,7 +905,7 @@ static int bn_bwd_impl(const void* dy, const uint8_t* mask, const void* x, int M
   hipLaunchKernelGGL((reduce_kernel<T, 1>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)dy,
                      mask, mean, M, C, p.chunk, part);
   SQR_HIP_LAUNCH_CHECK("bn bwd reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel");
   const int nvec = M * (C / 8);
@@ -966,7 +1015,7 @@ static int stem_bwd_impl(const void* dpool, const void* ypool, const uint8_t* ar
                      (const T*)dpool, (const T*)ypool, arg, (const T*)x, mean, N, H, W, C, Ho, Wo, chunk,
                      make_fastdiv(Wo), make_fastdiv(Ho), part);
   SQR_HIP_LAUNCH_CHECK("stem_bwd_reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel, dim3(C), dim3(256), 0, st, part, nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, bcoef);
   SQR_HIP_LAUNCH_CHECK("stem bwd_finalize_kernel");
   hipLaunchKernelGGL((stem_bwd_apply_kernel<T>), dim3(ew_grid(nqv)), dim3(256), 0, st, (const T*)dpool,
@@ -1174,4 +1223,64 @@ extern "C" int sqr_bn_add_bwd(const sqr_bn_operand* a, const sqr_bn_operand* b, 
                                 workspace, st);
   return bn_add_bwd_impl<float>(a, b, dy, relu_mask, (int)M, C, dx_a, dx_b, dgamma_a, dbeta_a, dgamma_b, dbeta_b,
                                 workspace, st);
+}
+
+// ---------------------------------------------------------------- backward from dgrad-epilogue partials
+int sqr::bn_mask_reduce(void* g, const void* x, const uint8_t* mask, const float* mean, long long M, int C, int dtype,
+                        float* stats, int* stats_rows, hipStream_t st) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  const RedPlan p = red_plan((int)M, C);
+  if (dtype == SQR_DTYPE_BF16)
+    hipLaunchKernelGGL((mask_reduce_kernel<bf16>), dim3(p.nblk), dim3(256), p.lds, st, (bf16*)g, (const bf16*)x, mask,
+                       mean, (int)M, C, p.chunk, stats);
+  else if (dtype == SQR_DTYPE_F16)
+    hipLaunchKernelGGL((mask_reduce_kernel<f16>), dim3(p.nblk), dim3(256), p.lds, st, (f16*)g, (const f16*)x, mask,
+                       mean, (int)M, C, p.chunk, stats);
+  else
+    hipLaunchKernelGGL((mask_reduce_kernel<float>), dim3(p.nblk), dim3(256), p.lds, st, (float*)g, (const float*)x,
+                       mask, mean, (int)M, C, p.chunk, stats);
+  SQR_HIP_LAUNCH_CHECK("bn mask_reduce_kernel");
+  *stats_rows = p.nblk;
+  return 0;
+}
+
+size_t sqr::bn_mask_reduce_rows(long long M, int C) { return (size_t)red_plan((int)M, C).nblk; }
+
+template <typename T>
+static int bn_bwd_stats_impl(const void* g, const void* x, int M, int C, const float* stats, int rows,
+                             const float* gamma, const float* mean, const float* invstd, void* dx, float* dgamma,
+                             float* dbeta, void* ws, hipStream_t st) {
+  float* coef = (float*)ws;
+  hipLaunchKernelGGL(bwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, stats, rows, M, C, gamma, mean, invstd,
+                     dgamma, dbeta, coef);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel(stats)");
+  const int nvec = M * (C / 8);
+  hipLaunchKernelGGL((bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)g,
+                     (const uint8_t*)nullptr, (const T*)x, coef, C, nvec, (T*)dx, (T*)nullptr);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_apply_kernel(stats)");
+  return 0;
+}
+
+extern "C" int sqr_bn_bwd_stats(const void* g, const void* x, long long M, int C, int dtype, const float* stats,
+                                int stats_rows, const float* gamma, const float* save_mean, const float* save_invstd,
+                                void* dx, float* dgamma, float* dbeta, void* workspace, size_t workspace_bytes,
+                                void* stream) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(g && x && stats && stats_rows > 0 && save_mean && save_invstd && dx && workspace,
+                "bn_bwd_stats: null pointer");
+  if (workspace_bytes < (size_t)3 * C * sizeof(float)) {
+    set_error("bn_bwd_stats: workspace too small");
+    return SQR_E_WORKSPACE;
+  }
+  hipStream_t st = as_stream(stream);
+  if (dtype == SQR_DTYPE_BF16)
+    return bn_bwd_stats_impl<bf16>(g, x, (int)M, C, stats, stats_rows, gamma, save_mean, save_invstd, dx, dgamma,
+                                   dbeta, workspace, st);
+  if (dtype == SQR_DTYPE_F16)
+    return bn_bwd_stats_impl<f16>(g, x, (int)M, C, stats, stats_rows, gamma, save_mean, save_invstd, dx, dgamma,
+                                  dbeta, workspace, st);
+  return bn_bwd_stats_impl<float>(g, x, (int)M, C, stats, stats_rows, gamma, save_mean, save_invstd, dx, dgamma,
+                                  dbeta, workspace, st);
 }

@@ -37,6 +37,10 @@ unsigned long long* probe_clock_take();
 int bn_finalize_partials(const float* part, int rows, long long M, int C, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* save_mean, float* save_invstd,
                          float* coef, hipStream_t st);
+// g *= mask in place + f32 (sum g, sum g*(x - mean)) partial rows (sqr_conv2d_bwd_data_bn fallback)
+int bn_mask_reduce(void* g, const void* x, const uint8_t* mask, const float* mean, long long M, int C, int dtype,
+                   float* stats, int* stats_rows, hipStream_t st);
+size_t bn_mask_reduce_rows(long long M, int C);
 int bn_infer_coef(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
                   float* coef, hipStream_t st);
 

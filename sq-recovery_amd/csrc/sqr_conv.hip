@@ -1225,6 +1225,41 @@ extern "C" int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void*
   return bwd_data_impl(dy, w_crsk, dx, addend, d, stream);
 }
 
+extern "C" size_t sqr_conv2d_bwd_data_bn_stats_floats(const sqr_conv_desc* d) {
+  Shape sh;
+  if (check_desc(d, &sh)) return 0;
+  const long long M = (long long)d->N * d->H * d->W;
+  size_t rows = (size_t)((M + 63) / 64);
+  const size_t rf = bn_mask_reduce_rows(M, d->C);
+  rows = rows < rf ? rf : rows;
+  rows = rows < 1024 ? 1024 : rows;
+  return rows * 2 * d->C;
+}
+
+extern "C" int sqr_conv2d_bwd_data_bn(const void* dy, const void* w_crsk, void* g_out, const void* bn_x,
+                                      const uint8_t* relu_mask, const float* bn_mean, float* stats, int* stats_rows,
+                                      const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  Shape sh;
+  int rc = check_desc(d, &sh);
+  if (rc) return rc;
+  SQR_CHECK_ARG(!sh.im2col, "conv2d_bwd_data_bn: C=%d < 8 not supported", d->C);
+  SQR_CHECK_ARG(dy && w_crsk && g_out && bn_x && relu_mask && bn_mean && stats && stats_rows,
+                "conv2d_bwd_data_bn: null pointer");
+  hipStream_t st = as_stream(stream);
+  if (direct3(d, sh)) {
+    const BnbArgs bnb = {bn_x, relu_mask, bn_mean};
+    rc = conv3_launch(d->dtype, dy, w_crsk, g_out, d->N, d->H, d->W, d->K, d->C, 1, stats, stats_rows, st, nullptr,
+                      &bnb);
+    if (rc != kNotHandled) return rc;
+  }
+  rc = bwd_data_impl(dy, w_crsk, g_out, nullptr, d, stream);
+  if (rc) return rc;
+  return bn_mask_reduce(g_out, bn_x, relu_mask, bn_mean, (long long)d->N * d->H * d->W, d->C, d->dtype, stats,
+                        stats_rows, st);
+}
+
 // implicit-GEMM backward-data over the output parity classes
 static int bwd_data_gemm(const void* dy, const void* w_crsk, void* dx, const sqr_conv_desc* d, const Shape& sh,
                          hipStream_t st) {

@@ -42,6 +42,9 @@ struct D3Args {
   const void* w;    // [Nout][9][Cin]
   void* out;        // [N][H][W][Nout]
   const void* addend;  // nullable: out = conv + addend ([N][H][W][Nout], may alias out)
+  const void* bn_x;        // BNB: the following BatchNorm's input [N][H][W][Nout], its ReLU mask and
+  const uint8_t* bn_mask;  //      batch mean: out = conv * mask, stats = (sum g, sum g*(x - mean))
+  const float* bn_mean;
   float* stats;     // nullable: BatchNorm partials [ntm][2][Nout]
   int N, H, W, Cin, Nout;
   int tiles_x, tiles_per_img;
@@ -127,8 +130,11 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 // ACC (backward-data of a block input): out = conv + a.addend.  The addend is loaded into registers
 // before the first DMA of the kernel, so its HBM read overlaps the main loop instead of adding a
 // burst at the end (measured at B=64: +3.9 us on layer 2 when read in the epilogue).
+// BNB (backward-data into a BatchNorm+ReLU backward): x and the mask bits at the lane's outputs are
+// loaded before the main loop like ACC's addend; the stored value is g = conv * mask and the tile's
+// partial row of a.stats gets the BatchNorm backward sums (sum g, sum g*(x - mean)).
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2,
-          bool ACC = false>
+          bool ACC = false, bool BNB = false>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
   constexpr int ROWB = 128, STAGES = PD + 1;
@@ -164,14 +170,18 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     const int ii = m / (TH * TW), mm = m - ii * (TH * TW);
     return (((size_t)(img + ii) * a.H + h0 + mm / TW) * a.W + w0 + (mm % TW)) * a.Nout + n0 + wn * WN + 4 * fq;
   };
-  u32x2 av[ACC ? TN : 1][ACC ? TM : 1];
-  if constexpr (ACC) {
-    const uint16_t* ad = (const uint16_t*)a.addend;
+  u32x2 av[ACC || BNB ? TN : 1][ACC || BNB ? TM : 1];
+  uint32_t bmk[BNB ? TN : 1][BNB ? TM : 1];
+  if constexpr (ACC || BNB) {
+    const uint16_t* ad = (const uint16_t*)(BNB ? a.bn_x : a.addend);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const size_t o = out_off(i);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) av[j][i] = *(const u32x2*)(ad + o + 16 * j);
+      for (int j = 0; j < TN; ++j) {
+        av[j][i] = *(const u32x2*)(ad + o + 16 * j);
+        if constexpr (BNB) bmk[j][i] = a.bn_mask[(o + 16 * j) >> 3];
+      }
     }
   }
 
@@ -358,12 +368,41 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       pk[j][i][0] = pack2<T>(acc[j][i][0], acc[j][i][1]);
       pk[j][i][1] = pack2<T>(acc[j][i][2], acc[j][i][3]);
     }
+  if constexpr (BNB) {  // g = conv * mask (4 channels of the lane: mask bits (opix & 4) .. +3)
+    float s1[TN][4], s2[TN][4], mu[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[j][e] = s2[j][e] = 0.f;
+        mu[j][e] = a.bn_mean[n0 + wn * WN + 16 * j + 4 * fq + e];
+      }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const uint32_t mb = (bmk[j][i] >> ((opix[i] + 16 * j) & 4)) & 0xfu;
+        pk[j][i][0] &= ((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u);
+        pk[j][i][1] &= ((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float g0 = lo2f<T>(pk[j][i][h]), g1 = hi2f<T>(pk[j][i][h]);
+          s1[j][2 * h] += g0;
+          s2[j][2 * h] = fmaf(g0, lo2f<T>(av[j][i][h]) - mu[j][2 * h], s2[j][2 * h]);
+          s1[j][2 * h + 1] += g1;
+          s2[j][2 * h + 1] = fmaf(g1, hi2f<T>(av[j][i][h]) - mu[j][2 * h + 1], s2[j][2 * h + 1]);
+        }
+      }
+    stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(s1, s2, (float*)smem, wm, wn, fr, fq, tid,
+                                               a.stats + ((size_t)tile_m * 2) * a.Nout + n0,
+                                               a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
+  }
   uint16_t* out = (uint16_t*)a.out;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) *(u32x2*)(out + opix[i] + 16 * j) = u32x2{pk[j][i][0], pk[j][i][1]};
-  if (a.stats)
+  if (!BNB && a.stats)
     tile_stats<T, BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
                                                  a.stats + ((size_t)tile_m * 2) * a.Nout + n0,
                                                  a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
@@ -386,6 +425,9 @@ struct D3PArgs {
   const void* w;   // [64][9][64]
   void* out;       // [N][H][64][64]
   const void* addend;  // ACC launches: out = conv + addend (backward-data of a block input; may alias out)
+  const void* bn_x;        // BNB launches: the following BatchNorm's input x [N][H][64][64] ...
+  const uint8_t* bn_mask;  // ... its ReLU mask (1 bit / element) and ...
+  const float* bn_mean;    // ... its batch mean: out = dgrad * mask, stats = its backward sums
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
   int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
@@ -404,6 +446,9 @@ __device__ __forceinline__ void wait_vm(int n) {
     case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
     case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -415,7 +460,11 @@ __device__ __forceinline__ void wait_vm(int n) {
 // at the start of iteration k+1, so its latency hides behind a whole tile of MFMA work; to keep
 // the compiler's wait for those registers from also waiting on just-issued row loads, ACC
 // launches store the previous tile BEFORE issuing the next rows.
-template <typename T, bool STATS, bool ACC = false>
+// BNB (backward-data feeding a BatchNorm+ReLU backward: a BasicBlock's conv2 dgrad into bn1): the
+// stored value is g = dgrad * [relu mask] and a.stats receives, per workgroup, the BatchNorm
+// backward sums (sum g, sum g*(x - mean)) — what sqr_bn_bwd's separate reduction pass would read
+// back.  x and the mask of tile k are prefetched like ACC's addend.
+template <typename T, bool STATS, bool ACC = false, bool BNB = false>
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
   // 2 x 2 waves, each 64 pixels (one image row) x 32 channels = two 32x32 MFMA accumulators
@@ -494,11 +543,25 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) st1[e] = st2[e] = 0.f;
 
-  u32x4 av[NST];  // ACC: the addend pieces of the tile stored next
+  u32x4 av[NST];  // ACC: the addend pieces of the tile stored next; BNB: the BatchNorm input x there
+  uint32_t bm[BNB ? NST : 1];  // BNB: the mask byte of each piece (8 channels)
+  float bs1[BNB ? 8 : 1], bs2[BNB ? 8 : 1], bmu[BNB ? 8 : 1];  // BNB: this thread's 8 channels (tid & 7)
+  if constexpr (BNB) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bs1[e] = bs2[e] = 0.f;
+      bmu[e] = a.bn_mean[(tid & 7) * 8 + e];
+    }
+  }
   auto load_addend = [&](int k) {
-    const char* src = (const char*)a.addend + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
+    const size_t tile0 = ((size_t)img * H + hb + k * TH) * TW * BN;  // first element of tile k
+    const char* src = (const char*)(BNB ? a.bn_x : a.addend) + tile0 * 2;
 #pragma unroll
     for (int q = 0; q < NST; ++q) av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
+    if constexpr (BNB) {
+#pragma unroll
+      for (int q = 0; q < NST; ++q) bm[q] = a.bn_mask[tile0 / 8 + q * NT + tid];
+    }
   };
   auto store_staged = [&](int k) {
     char* dst = (char*)a.out + ((size_t)img * H + hb + k * TH) * TW * BN * 2;
@@ -510,6 +573,18 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           v[e] = pack2<T>(lo2f<T>(v[e]) + lo2f<T>(av[q][e]), hi2f<T>(v[e]) + hi2f<T>(av[q][e]));
+      }
+      if constexpr (BNB) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t keep = (((bm[q] >> (2 * e)) & 1u) ? 0xffffu : 0u) | (((bm[q] >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u);
+          v[e] &= keep;  // g = dgrad * mask (masked halves become +0)
+          const float g0 = lo2f<T>(v[e]), g1 = hi2f<T>(v[e]);
+          bs1[2 * e] += g0;
+          bs2[2 * e] = fmaf(g0, lo2f<T>(av[q][e]) - bmu[2 * e], bs2[2 * e]);
+          bs1[2 * e + 1] += g1;
+          bs2[2 * e + 1] = fmaf(g1, hi2f<T>(av[q][e]) - bmu[2 * e + 1], bs2[2 * e + 1]);
+        }
       }
 #if SQR_EXP & 256
       if (v[0] == 0x12345678u && v[1] == 0x9abcdef0u) *(u32x4*)(dst + (size_t)c * 16) = v;
@@ -527,7 +602,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   for (int k = 0; k < ntile; ++k) {
     // tile k+2's new rows go into the slots tile k-1 used (free since the last barrier)
     int pn;
-    if constexpr (ACC) {
+    if constexpr (ACC || BNB) {
       if (k >= 1) store_staged(k - 1);
       pn = k + 2 < ntile ? issue_rows(hb + 2 * (k + 2) + 1, 2) : 0;
       load_addend(k);
@@ -611,6 +686,8 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     // loads of tile k-1, the stores of tile k-1, the row loads of tile k+2, the addend loads of k)
     if constexpr (ACC)
       wait_vm(pn + (k >= 1 ? 2 * NST : 0) + NST);
+    else if constexpr (BNB)  // per tile: NST x loads + NST mask-byte loads
+      wait_vm(pn + (k >= 1 ? 3 * NST : 0) + 2 * NST);
     else
       wait_vm(pn + (k >= 1 ? NST : 0) + (k >= 2 ? NST : 0));
     __builtin_amdgcn_s_barrier();  // ... for every wave; all waves are done with tile k's rows and the staging area
@@ -627,6 +704,23 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     __builtin_amdgcn_s_barrier();  // staged tile visible
   }
   if (ntile > 0) store_staged(ntile - 1);
+  if constexpr (BNB) {  // red[256 threads][16] -> per channel, the 32 threads of its slot in order
+    __syncthreads();
+    float* red = (float*)ring;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[tid * 16 + e] = bs1[e];
+      red[tid * 16 + 8 + e] = bs2[e];
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int q = tid / BN, col = tid - q * BN, sl = col >> 3, e = col & 7;
+      float sum = 0.f;
+#pragma unroll 8
+      for (int i = 0; i < NT / 8; ++i) sum += red[(sl + 8 * i) * 16 + 8 * q + e];
+      a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = sum;
+    }
+  }
   if (STATS && !(SQR_EXP & 32768)) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
     __syncthreads();
     float* red = (float*)ring;
@@ -1255,7 +1349,7 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
 
 // kNotHandled = not applicable (caller falls back to the implicit-GEMM path), 0 = launched, else error
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
-                 float* stats, int* stats_rows, hipStream_t st, const void* addend) {
+                 float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb) {
   if (g_direct == 0) return kNotHandled;
   if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return kNotHandled;
   const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
@@ -1277,6 +1371,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     p.w = w;
     p.out = out;
     p.addend = addend;
+    p.bn_x = bnb ? bnb->x : nullptr;
+    p.bn_mask = bnb ? bnb->mask : nullptr;
+    p.bn_mean = bnb ? bnb->mean : nullptr;
     p.stats = stats;
     p.H = H;
     p.bpi = bpi;
@@ -1289,7 +1386,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
     probe_begin(st);
     SQR_DISPATCH16(dtype, T, {
-      if (stats)
+      if (bnb)
+        hipLaunchKernelGGL((conv3p_kernel<T, false, false, true>), dim3(grid), dim3(256), 0, st, p);
+      else if (stats)
         hipLaunchKernelGGL((conv3p_kernel<T, true>), dim3(grid), dim3(256), 0, st, p);
       else if (addend)
         hipLaunchKernelGGL((conv3p_kernel<T, false, true>), dim3(grid), dim3(256), 0, st, p);
@@ -1307,6 +1406,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   a.w = w;
   a.out = out;
   a.addend = addend;
+  a.bn_x = bnb ? bnb->x : nullptr;
+  a.bn_mask = bnb ? bnb->mask : nullptr;
+  a.bn_mean = bnb ? bnb->mean : nullptr;
   a.stats = stats;
   a.N = N;
   a.H = H;
@@ -1324,25 +1426,27 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   if (stats_rows) *stats_rows = a.ntm;
   const dim3 grid(a.ntm * a.ntn), blk(c.threads);
   probe_begin(st);
-#define SQR_D3_CASES(ACC_)                                                                                         \
+#define SQR_D3_CASES(ACC_, BNB_)                                                                                   \
   switch (c.id) {                                                                                                  \
-    case 0: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 64, 4, 1, 1, 2, ACC_>), grid, blk, 0, st, a); break;    \
-    case 1: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;   \
-    case 2: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;   \
-    case 3: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;     \
-    case 4: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 16, 16, 2, 1, 2, ACC_>), grid, blk, 0, st, a); break;   \
-    case 5: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 2, ACC_>), grid, blk, 0, st, a); break;     \
-    case 6: hipLaunchKernelGGL((conv3_kernel<T, 256, 32, 4, 1, 8, 8, 2, 4, 2, ACC_>), grid, blk, 0, st, a); break;     \
-    case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 3, ACC_>), grid, blk, 0, st, a); break;   \
-    case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5, ACC_>), grid, blk, 0, st, a); break;   \
-    case 9: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 5, ACC_>), grid, blk, 0, st, a); break;     \
-    default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8, ACC_>), grid, blk, 0, st, a); break;    \
+    case 0: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 64, 4, 1, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;    \
+    case 1: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
+    case 2: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
+    case 3: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;     \
+    case 4: hipLaunchKernelGGL((conv3_kernel<T, 256, 64, 4, 1, 16, 16, 2, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
+    case 5: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;     \
+    case 6: hipLaunchKernelGGL((conv3_kernel<T, 256, 32, 4, 1, 8, 8, 2, 4, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;     \
+    case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 3, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
+    case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
+    case 9: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 5, ACC_, BNB_>), grid, blk, 0, st, a); break;     \
+    default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8, ACC_, BNB_>), grid, blk, 0, st, a); break;    \
   }
   SQR_DISPATCH16(dtype, T, {
-    if (addend) {
-      SQR_D3_CASES(true)
+    if (bnb) {
+      SQR_D3_CASES(false, true)
+    } else if (addend) {
+      SQR_D3_CASES(true, false)
     } else {
-      SQR_D3_CASES(false)
+      SQR_D3_CASES(false, false)
     }
   });
 #undef SQR_D3_CASES

@@ -152,9 +152,18 @@ constexpr int kNotHandled = -1000;
 
 // direct 3x3/s1/p1 bf16 / fp16 kernel (sqr_conv3.hip): kNotHandled = shape not handled (use the
 // implicit-GEMM path), 0 = launched, otherwise an error code
-// addend (nullable, backward-data only): out = conv + addend, fused into the epilogue
+// the following BatchNorm's operands for a backward-data launch that feeds its backward (BNB):
+// the stored value becomes dgrad * mask and stats receives (sum g, sum g*(x - mean)) partial rows
+struct BnbArgs {
+  const void* x;
+  const uint8_t* mask;
+  const float* mean;
+};
+// addend (nullable, backward-data only): out = conv + addend, fused into the epilogue;
+// bnb (nullable, backward-data only): see BnbArgs (stats / stats_rows then receive its partials)
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
-                 float* stats, int* stats_rows, hipStream_t st, const void* addend = nullptr);
+                 float* stats, int* stats_rows, hipStream_t st, const void* addend = nullptr,
+                 const BnbArgs* bnb = nullptr);
 // direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,

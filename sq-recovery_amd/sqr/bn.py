@@ -36,7 +36,7 @@ def _ws_bytes(M, C):
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps, stats=None,
-                res_join=None):
+                res_join=None, link=None):
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
@@ -65,6 +65,10 @@ class BNActFn(torch.autograd.Function):
         ctx.relu, ctx.training, ctx.eps = relu, training, eps
         ctx.has_res = residual is not None
         ctx.res_join = res_join  # sqr.conv.ResidualJoin of the residual input: its gradient is deposited
+        # sqr.conv.BnBackwardLink: the consuming conv's backward-data computes this BN's reduction
+        ctx.link = link if (training and relu and residual is None and mask is not None) else None
+        if ctx.link is not None:
+            ctx.link.x, ctx.link.mask, ctx.link.mean = x, mask, mean
         ctx.pids = (id(weight), id(bias))
         if training:
             ctx.save_for_backward(x, mask, weight, mean, invstd)
@@ -86,13 +90,22 @@ class BNActFn(torch.autograd.Function):
             dres = g.to(x.dtype) if ctx.has_res else None
             if ctx.res_join is not None:
                 dres = ctx.res_join.deposit(dres)
-            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None, None
+            return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None, None, \
+                None
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
         dgamma = gradbuf.out(ctx.pids[0], (C,), x.device)
         dbeta = gradbuf.out(ctx.pids[1], (C,), x.device)
         n = _ws_bytes(M, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        got = ctx.link.take(dy) if ctx.link is not None else None
+        if got is not None:  # the consuming conv's backward-data already masked g and reduced it
+            g, st = got
+            check(lib().sqr_bn_bwd_stats(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(st), st.shape[0],
+                                         ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n,
+                                         stream_ptr(x.device)), "sqr_bn_bwd_stats")
+            gradbuf.written(ctx.pids)
+            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
         check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
@@ -101,7 +114,7 @@ class BNActFn(torch.autograd.Function):
             dres = dy
         if ctx.res_join is not None:
             dres = ctx.res_join.deposit(dres)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
 
 
 def count_batches(bns):
@@ -127,11 +140,12 @@ def _check_stats(stats, x):
     return stats
 
 
-def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None):
+def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=None):
     """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics.
     x may be a (y, partials) pair from a stats-producing conv: training mode then takes the batch
     statistics from the partials instead of reducing over y.  res_join: the residual input's
-    sqr.conv.ResidualJoin (its gradient goes there instead of to autograd)."""
+    sqr.conv.ResidualJoin (its gradient goes there instead of to autograd); link: a
+    sqr.conv.BnBackwardLink to the conv that consumes the output (see there)."""
     x, stats = _split(x)
     training = bn.training or not bn.track_running_stats
     if training and bn.track_running_stats and not counted:
@@ -140,7 +154,7 @@ def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None):
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
-                         _check_stats(stats, x), res_join if residual is not None else None)
+                         _check_stats(stats, x), res_join if residual is not None else None, link)
 
 
 def _operand(x, stats, weight, bias, rmean, rvar, momentum, eps, mean, invstd):

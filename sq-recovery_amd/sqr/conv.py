@@ -249,6 +249,55 @@ def conv2d_bwd_data_acc(gy, w_crsk, d, addend):
     return dx
 
 
+def conv2d_bwd_data_bn(gy, w_crsk, d, bn_x, bn_mask, bn_mean):
+    """(g, partials): g = bwd_data(gy) * bn_mask and the following BatchNorm's backward sums
+    [rows, 2, C] (sqr_conv2d_bwd_data_bn: the direct kernels compute both in their epilogues)."""
+    import ctypes
+    dt = _TORCH_DT[d.dtype]
+    g = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=gy.device, memory_format=_CL)
+    L = lib()
+    st = torch.empty(L.sqr_conv2d_bwd_data_bn_stats_floats(ctypes.byref(d)), dtype=torch.float32, device=gy.device)
+    rows = ctypes.c_int()
+    ws, n = _ws(d, 1, gy.device)
+    with _Probe("dgrad", d):
+        rc = L.sqr_conv2d_bwd_data_bn(ptr(gy), ptr(w_crsk), ptr(g), ptr(bn_x), ptr(bn_mask), ptr(bn_mean), ptr(st),
+                                      ctypes.byref(rows), ctypes.byref(d), ptr(ws), n, stream_ptr(gy.device))
+    check(rc, "sqr_conv2d_bwd_data_bn")
+    return g, st[:rows.value * 2 * d.C].view(rows.value, 2, d.C)
+
+
+class BnBackwardLink:
+    """bn1 -> relu -> conv2 of a BasicBlock (torch/models.py:181): conv2's backward-data also
+    produces bn1's backward reduction (sqr_conv2d_bwd_data_bn), so bn1's backward skips its own pass
+    over (g, x).  bn1's forward fills x / mask / mean; conv2's backward fills g / stats; bn1's
+    backward uses them only if the gradient it receives IS that g (conv2 is the relu output's only
+    consumer in a BasicBlock), otherwise it runs its own reduction (masking an already-masked g is
+    harmless)."""
+
+    __slots__ = ("x", "mask", "mean", "g", "stats")
+
+    def __init__(self):
+        self.x = self.mask = self.mean = self.g = self.stats = None
+
+    @staticmethod
+    def make(x, bn):
+        if x.is_cuda and torch.is_grad_enabled() and bn.training and x.dtype in (torch.bfloat16, torch.float16,
+                                                                                 torch.float32):
+            return BnBackwardLink()
+        return None
+
+    def ready(self):
+        return self.x is not None and self.mask is not None and self.mean is not None
+
+    def take(self, dy):
+        """(g, stats) if dy is the g this link's conv produced, else None; clears the link."""
+        g, st = self.g, self.stats
+        self.g = self.stats = None
+        if g is None or st is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
+            return None
+        return g, st
+
+
 class ResidualJoin:
     """The two gradient contributions of a residual block's input x (torchvision BasicBlock:
     x feeds conv1 AND the identity / downsample branch, torch/models.py:181) summed without a
@@ -302,7 +351,7 @@ def compute_dtype(x):
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False, join=None, role=None):
+    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False, join=None, role=None, bnb=None):
         # the statistics output is non-differentiable: don't let autograd materialise a zero
         # gradient tensor for it in backward
         ctx.set_materialize_grads(False)
@@ -324,6 +373,7 @@ class Conv2dFn(torch.autograd.Function):
             y = y + bias.to(dt).view(1, K, 1, 1)
         ctx.d = d
         ctx.join, ctx.role = join, role  # ResidualJoin of x: role "acc" (conv1) / "dep" (downsample)
+        ctx.bnb = bnb  # BnBackwardLink of x's BatchNorm (bn1 -> relu -> this conv)
         ctx.wid = id(weight)
         ctx.x_dtype = x.dtype
         ctx.has_bias = bias is not None
@@ -339,7 +389,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, *_):
         if gy is None:  # grads are not materialised (see forward)
-            return (None,) * 10
+            return (None,) * 11
         xin, crsk, col = ctx.saved_tensors
         d = ctx.d
         dt = _TORCH_DT[d.dtype]
@@ -349,7 +399,11 @@ class Conv2dFn(torch.autograd.Function):
             if crsk is None:
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
             addend = ctx.join.take() if (ctx.join is not None and ctx.role == "acc") else None
-            if addend is not None and addend.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W) \
+            link = ctx.bnb if (ctx.bnb is not None and ctx.bnb.ready() and addend is None) else None
+            if link is not None and link.x.dtype == dt:
+                dx, link.stats = conv2d_bwd_data_bn(g, crsk, d, link.x, link.mask, link.mean)
+                link.g = dx
+            elif addend is not None and addend.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W) \
                     and addend.is_contiguous(memory_format=_CL):
                 dx = conv2d_bwd_data_acc(g, crsk, d, addend)
             else:
@@ -364,17 +418,17 @@ class Conv2dFn(torch.autograd.Function):
             gradbuf.written((ctx.wid,))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False, join=None, role=None):
+def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False, join=None, role=None, bnb=None):
     """conv(x); with stats=True returns (y, partials) where partials feed the following
     BatchNorm (sqr.bn.bn_act / stem ``stats=``) so it skips its statistics pass over y
     (partials is None when the conv has a bias)."""
     if not x.is_cuda:
         raise ValueError("sqr conv2d runs on MI355X; got a %s tensor" % x.device)
     return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed, bool(stats), join,
-                          role)
+                          role, bnb)
 
 
 class Conv2d(nn.Conv2d):
@@ -401,7 +455,7 @@ class Conv2d(nn.Conv2d):
             return super().forward(x)
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x))
 
-    def forward_stats(self, x, bn=None, join=None, role=None):
+    def forward_stats(self, x, bn=None, join=None, role=None, bnb=None):
         """(y, BatchNorm partials of y) — see conv2d(stats=True).  With `bn` given, the partials
         are produced only when that BatchNorm will use batch statistics (else y alone).  join/role:
         a ResidualJoin of x (see there)."""
@@ -409,4 +463,4 @@ class Conv2d(nn.Conv2d):
             return self.forward(x)
         want = bn is None or bn.training or not bn.track_running_stats
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x), stats=want,
-                      join=join, role=role)
+                      join=join, role=role, bnb=bnb)

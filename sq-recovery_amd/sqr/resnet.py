@@ -13,14 +13,16 @@ import torch
 import torch.nn as nn
 
 from .bn import bn_act, bn_add_act, count_batches, fused_stem, fused_stem_ok, stem
-from .conv import Conv2d, ResidualJoin, compute_dtype, pack_all
+from .conv import BnBackwardLink, Conv2d, ResidualJoin, compute_dtype, pack_all
 
 
 # ablation switches (A/B timing in one process / on one box; both default on):
 #   SQR_RESIDUAL_JOIN=0  the residual branch's gradient goes back through autograd's add
 #   SQR_BN_ADD=0         bn2 + downsample-bn as two BatchNorm ops (the identity tensor is written)
+#   SQR_BN_LINK=0        bn1's backward reduction as its own pass (not in conv2's dgrad epilogue)
 _JOIN = os.environ.get("SQR_RESIDUAL_JOIN", "1") != "0"
 _BN_ADD = os.environ.get("SQR_BN_ADD", "1") != "0"
+_BN_LINK = os.environ.get("SQR_BN_LINK", "1") != "0"
 
 
 class BasicBlock(nn.Module):
@@ -46,19 +48,21 @@ class BasicBlock(nn.Module):
         # the identity / downsample branch's gradient of x is added in conv1's backward-data
         # epilogue through a ResidualJoin instead of a separate add)
         join = ResidualJoin.make(x) if _JOIN else None
-        out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc"), self.bn1, relu=True, counted=True)
+        link = BnBackwardLink.make(x, self.bn1) if _BN_LINK else None
+        out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc"), self.bn1, relu=True, counted=True,
+                     link=link)
         if self.downsample is not None and not _BN_ADD:
             identity = bn_act(self.downsample[0].forward_stats(x, self.downsample[1], join=join, role="dep"),
                               self.downsample[1], relu=False, counted=True)
-            return bn_act(self.conv2.forward_stats(out, self.bn2), self.bn2, residual=identity, relu=True,
+            return bn_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, residual=identity, relu=True,
                           counted=True)
         if self.downsample is not None:
             # bn2(conv2) + bn_ds(conv_ds) + ReLU as ONE op: the downsample branch is never normalised
             # into a tensor of its own (sqr_bn_add_*)
             ds = self.downsample[0].forward_stats(x, self.downsample[1], join=join, role="dep")
-            return bn_add_act(self.conv2.forward_stats(out, self.bn2), self.bn2, ds, self.downsample[1],
+            return bn_add_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, ds, self.downsample[1],
                               relu=True, counted=True)
-        return bn_act(self.conv2.forward_stats(out, self.bn2), self.bn2, residual=x, relu=True, counted=True,
+        return bn_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, residual=x, relu=True, counted=True,
                       res_join=join)
 
 

@@ -408,3 +408,48 @@ def test_conv_bwd_data_acc(shape, dtype):
     # the fused sum equals the separate sum up to one rounding of the 16-bit result
     assert _rel(dx, plain.double() + addg.double()) <= (1.0 if dtype == torch.float32 else 2.0) * tol
     assert torch.equal(addg.cpu().float(), add.to(dtype).float())  # the addend is not modified
+
+
+# ---------------------------------------------------------------- dgrad + BatchNorm-backward sums
+# sqr_conv2d_bwd_data_bn (a BasicBlock's conv2 backward-data feeding bn1's backward): g = dgrad * mask
+# and the per-channel sums (sum g, sum g*(x - mean)) — the persistent layer-1 kernel (ring wrap at
+# the bench batch), the tiled kernels of layers 2-4, and the implicit-GEMM fallback (fp32, odd size).
+BNB_SHAPES = [(4, 64, 64, 64), (64, 64, 64, 64), (4, 128, 32, 128), (64, 128, 32, 128), (4, 256, 16, 256),
+              (4, 512, 8, 512), (2, 64, 128, 64), (3, 32, 20, 32)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=["bf16", "f16", "f32"])
+@pytest.mark.parametrize("shape", BNB_SHAPES, ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv_bwd_data_bn(shape, dtype):
+    from sqr import conv as sc
+    N, C, H, K = shape
+    if dtype == torch.float32 and N > 8:
+        pytest.skip("fp32 runs the implicit GEMM + mask/reduce fallback; small batches cover it")
+    g = torch.Generator().manual_seed(5 * N + C + K + H)
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    gy = torch.randn(N, K, H, H, generator=g).to(dtype).float()
+    x = (torch.randn(N, C, H, H, generator=g) * 1.5 + 0.3).to(dtype).float()
+    keep = torch.rand(N, C, H, H, generator=g) > 0.4  # the BatchNorm's ReLU mask
+    mean = torch.randn(C, generator=g) * 0.2
+    # 1-bit mask in the NHWC element order, 8 channels per byte (bit i = channel 8v + i)
+    bits = keep.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.int64)
+    mask = (bits << torch.arange(8)).sum(1).to(torch.uint8)
+    d = sc._desc(N, C, H, H, K, 3, 3, 1, 1, dtype)
+    _, crsk = sc.pack_weight(w.to(DEV), d, True)
+    cl = dict(memory_format=torch.channels_last)
+    gg, st = sc.conv2d_bwd_data_bn(gy.to(DEV).to(dtype).contiguous(**cl), crsk, d, x.to(DEV).to(dtype).contiguous(**cl),
+                                   mask.to(DEV), mean.to(DEV))
+    plain = sc.conv2d_bwd_data(gy.to(DEV).to(dtype).contiguous(**cl), crsk, d)
+    torch.cuda.synchronize()
+    # g is exactly the plain 16-bit dgrad with the masked elements zeroed
+    assert torch.equal(gg.cpu(), (plain.cpu() * keep.to(plain.dtype)))
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.to(dtype).double(), gy.double(), stride=1, padding=1) * keep
+    tol = {torch.bfloat16: 8e-3, torch.float16: 1e-3, torch.float32: 1e-5}[dtype]
+    assert _rel(gg, ref) <= tol
+    # the sums are those of the stored g (f64 over the rows)
+    gd = gg.double().cpu()
+    s1 = gd.sum((0, 2, 3))
+    s2 = (gd * (x.double() - mean.double().view(1, C, 1, 1))).sum((0, 2, 3))
+    tot = st.double().sum(0).cpu()
+    assert st.shape[1:] == (2, C)
+    assert _rel(tot[0], s1) <= 1e-5 and _rel(tot[1], s2) <= 1e-5
