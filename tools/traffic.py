@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 # the probe kernel of bench.py (PROBE = fwd, layer1 3x3 64->64): the persistent direct conv, which
@@ -18,8 +19,18 @@ DEFAULT_KERNEL = "conv3p_kernel"
 PROBE_KEY = ["fwd", 64, 64, 3, 1]
 
 
+# the forward (statistics-producing) instance of the probe kernel: conv3p_kernel<T, STATS=true, ...>;
+# its backward-data instances (plain / + residual addend / + BatchNorm-backward operands) move
+# different bytes and are reported separately
+# (rocprofv3 leaves some instances mangled — STATS is the first bool: ...IDF16bLb1E... — and
+# demangles others badly: the forward bf16 instance shows as "conv3p_kernel<bool _Accum, bool, E,
+# false, false>", the type and STATS eaten; the two trailing flags ACC = BNB = false single it out
+# among this step's instances: forward, dgrad + addend, dgrad + BatchNorm operands)
+FWD_RE = re.compile(r"conv3p_kernel(IDF16b?Lb1E|<[^<>]*?,\s*true,|<bool _Accum, bool, E, false, false>)")
+
+
 def per_dispatch(root, counter, kernel):
-    vals = []
+    by = {}
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
@@ -27,8 +38,8 @@ def per_dispatch(root, counter, kernel):
                     continue
                 name = row.get("Kernel_Name", "")
                 if kernel in name:
-                    vals.append(float(row["Counter_Value"]))
-    return vals
+                    by.setdefault(name, []).append(float(row["Counter_Value"]))
+    return by
 
 
 def main():
@@ -36,13 +47,22 @@ def main():
     kernel = sys.argv[2] if len(sys.argv) > 2 else DEFAULT_KERNEL
     fetch = per_dispatch(os.path.join(out, "pmc_fetch"), "FETCH_SIZE", kernel)
     write = per_dispatch(os.path.join(out, "pmc_write"), "WRITE_SIZE", kernel)
-    res = {"kernel": kernel, "kernel_key": PROBE_KEY, "dispatches": [len(fetch), len(write)]}
-    if fetch and write:
-        f = sum(fetch) / len(fetch) * 1024.0 * 2.0  # KiB -> B, gfx950 half-count correction
-        w = sum(write) / len(write) * 1024.0
+    pick = [n for n in fetch if FWD_RE.search(n)] if kernel == DEFAULT_KERNEL else list(fetch)
+    if not pick:
+        pick = list(fetch)
+    fv = [v for n in pick for v in fetch.get(n, [])]
+    wv = [v for n in pick for v in write.get(n, [])]
+    res = {"kernel": kernel, "kernel_key": PROBE_KEY, "instances": pick, "dispatches": [len(fv), len(wv)]}
+    if fv and wv:
+        f = sum(fv) / len(fv) * 1024.0 * 2.0  # KiB -> B, gfx950 half-count correction
+        w = sum(wv) / len(wv) * 1024.0
         res.update({"fetch_bytes_per_launch": f, "write_bytes_per_launch": w,
                     "hbm_bytes_per_launch": f + w,
                     "note": "FETCH_SIZE x1024 x2 (gfx950 wide-read half count) + WRITE_SIZE x1024, mean over dispatches"})
+    res["by_kernel"] = {n: {"dispatches": len(fetch[n]),
+                            "fetch_bytes": sum(fetch[n]) / len(fetch[n]) * 2048.0,
+                            "write_bytes": (sum(write[n]) / len(write[n]) * 1024.0) if write.get(n) else None}
+                        for n in fetch}
     print(json.dumps(res, indent=1))
 
 
