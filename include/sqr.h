@@ -183,6 +183,24 @@ int sqr_conv2d_bwd_data_bn(const void* dy, const void* w_crsk, void* g_out, cons
 /* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
 int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* A BatchNorm backward finalize riding along a weight-gradient launch: the BatchNorm whose
+ * backward sums sqr_conv2d_bwd_data_bn produced (stats [stats_rows][2][C] f32, over M pixels) gets
+ * dgamma / dbeta and coef = [k1 C][k2 C][k3 C] for sqr_bn_bwd_apply, computed by extra workgroups
+ * of the weight gradient's split-K reduction instead of a launch of their own. */
+typedef struct sqr_bn_bwd_fin {
+  const float* stats;
+  int stats_rows;
+  long long M;
+  int C;
+  const float* gamma;       /* nullable (affine=False) */
+  const float* save_mean;
+  const float* save_invstd;
+  float* dgamma;            /* nullable */
+  float* dbeta;             /* nullable */
+  float* coef;              /* out, 3*C floats */
+} sqr_bn_bwd_fin;
+int sqr_conv2d_bwd_weight_bnfin(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                                const sqr_bn_bwd_fin* fin, void* workspace, size_t workspace_bytes, void* stream);
 /* C<8 (im2col) convs only: the same from the im2col matrix the forward left at the start of its
  * workspace (sqr_conv2d_workspace_bytes(d,0) bytes), skipping the re-gather; this call's own
  * workspace needs sqr_conv2d_workspace_bytes(d,2) - sqr_conv2d_workspace_bytes(d,0) bytes. */
@@ -218,6 +236,9 @@ int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* x, long lon
 int sqr_bn_bwd_stats(const void* g, const void* x, long long M, int C, int dtype, const float* stats, int stats_rows,
                      const float* gamma, const float* save_mean, const float* save_invstd, void* dx, float* dgamma,
                      float* dbeta, void* workspace, size_t workspace_bytes, void* stream);
+/* dx = k1*g + k3*x + k2 from finalized coefficients (sqr_conv2d_bwd_weight_bnfin's coef) */
+int sqr_bn_bwd_apply(const void* g, const void* x, long long M, int C, int dtype, const float* coef, void* dx,
+                     void* stream);
 
 /* Two-branch BatchNorm: y = act(bn_a(a.x) + bn_b(b.x)) — torchvision BasicBlock with a downsample,
  * relu(bn2(conv2(.)) + bn_ds(conv_ds(x))) (torch/models.py:181).  One apply pass reads both conv

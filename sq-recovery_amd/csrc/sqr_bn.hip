@@ -12,6 +12,7 @@
 //             -> dx = k1*g + k3*x + k2  (and dres = g for the residual branch)
 #include <stdint.h>
 #include "sqr_common.h"
+#include "sqr_bn_dev.h"
 
 namespace sqr {
 namespace bn {
@@ -160,32 +161,6 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
   }
 }
 
-// one block per channel: thread t sums partials t, t+256, ... (independent loads in flight), then a
-// fixed xor-tree wave reduction and a fixed-order sum of the 4 waves (deterministic).  Returns
-// true on thread 0 only.
-// (partials [k][NS][C]: statistic 0 and statistic SB of channel c)
-template <typename P, int NS = 2, int SB = 1>
-__device__ __forceinline__ bool sum_partials_c(const P* __restrict__ part, int nblk, int C, int c, double* s) {
-  __shared__ double red[2][4];
-  const int t = threadIdx.x;
-  double a = 0.0, b = 0.0;
-#pragma unroll 4
-  for (int k = t; k < nblk; k += 256) {
-    a += (double)part[(size_t)k * NS * C + c];
-    b += (double)part[(size_t)k * NS * C + SB * C + c];
-  }
-  a = wave_sum_d(a);
-  b = wave_sum_d(b);
-  if ((t & 63) == 0) {
-    red[0][t >> 6] = a;
-    red[1][t >> 6] = b;
-  }
-  __syncthreads();
-  if (t != 0) return false;
-  s[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-  s[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-  return true;
-}
 template <typename P>
 __device__ __forceinline__ bool sum_partials(const P* __restrict__ part, int nblk, int C, double* s, int* cout) {
   *cout = blockIdx.x;
@@ -275,19 +250,7 @@ __global__ void bwd_finalize_kernel(const P* __restrict__ part, int nblk, int M,
                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, float* __restrict__ dgamma,
                                     float* __restrict__ dbeta, float* __restrict__ coef) {
-  double acc[2];
-  int c;
-  if (!sum_partials(part, nblk, C, acc, &c)) return;
-  const double sg = acc[0], sgx = acc[1];
-  const double is = invstd[c], mu = mean[c];
-  const double dgam = sgx * is;  // sum g * xhat
-  if (dgamma) dgamma[c] = (float)dgam;
-  if (dbeta) dbeta[c] = (float)sg;
-  const double a = (gamma ? gamma[c] : 1.0) * is;
-  const double k3 = -a * is * dgam / M;
-  coef[c] = (float)a;
-  coef[2 * C + c] = (float)k3;
-  coef[C + c] = (float)(-a * sg / M - k3 * mu);
+  bn_bwd_finalize_c<P>(part, nblk, M, C, blockIdx.x, gamma, mean, invstd, dgamma, dbeta, coef);
 }
 
 // dx = k1*g + k3*x + k2 with g = dy*[relu bit]; optionally dres = g
@@ -1283,4 +1246,24 @@ extern "C" int sqr_bn_bwd_stats(const void* g, const void* x, long long M, int C
                                   dbeta, workspace, st);
   return bn_bwd_stats_impl<float>(g, x, (int)M, C, stats, stats_rows, gamma, save_mean, save_invstd, dx, dgamma,
                                   dbeta, workspace, st);
+}
+
+extern "C" int sqr_bn_bwd_apply(const void* g, const void* x, long long M, int C, int dtype, const float* coef,
+                                void* dx, void* stream) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(g && x && coef && dx, "bn_bwd_apply: null pointer");
+  hipStream_t st = as_stream(stream);
+  const int nvec = (int)M * (C / 8);
+  if (dtype == SQR_DTYPE_BF16)
+    hipLaunchKernelGGL((bwd_apply_kernel<bf16>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)g,
+                       (const uint8_t*)nullptr, (const bf16*)x, coef, C, nvec, (bf16*)dx, (bf16*)nullptr);
+  else if (dtype == SQR_DTYPE_F16)
+    hipLaunchKernelGGL((bwd_apply_kernel<f16>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const f16*)g,
+                       (const uint8_t*)nullptr, (const f16*)x, coef, C, nvec, (f16*)dx, (f16*)nullptr);
+  else
+    hipLaunchKernelGGL((bwd_apply_kernel<float>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const float*)g,
+                       (const uint8_t*)nullptr, (const float*)x, coef, C, nvec, (float*)dx, (float*)nullptr);
+  SQR_HIP_LAUNCH_CHECK("bn bwd_apply_kernel(coef)");
+  return 0;
 }

@@ -29,6 +29,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include "sqr_conv_dev.h"
+#include "sqr_bn_dev.h"
 
 namespace sqr {
 namespace conv {
@@ -565,9 +566,17 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 // with 8 independent 16-B loads in flight (the pass is HBM/MALL-bound and needs the bytes in
 // flight), then the ZL partial sums are added in a fixed order through LDS -> deterministic.
 // The permuted writes to torch's KCRS layout are 4-B scatters (the output is small).
+// Workgroups past the reduction's own (blockIdx.x >= nred) finalize a BatchNorm backward instead
+// (fin, one channel each): the BatchNorm whose backward sums this conv's backward-data epilogue
+// produced rides along this launch instead of taking one of its own.
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int zl_log2,
                                                            int K, int Ng, int C, int R, int S, int Ci, int im2col,
-                                                           float* __restrict__ dw) {
+                                                           float* __restrict__ dw, int nred, bn::BnFinDev fin) {
+  if ((int)blockIdx.x >= nred) {
+    bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, blockIdx.x - nred, fin.gamma, fin.mean, fin.invstd,
+                                 fin.dgamma, fin.dbeta, fin.coef);
+    return;
+  }
   __shared__ f32x4 part[256];
   const int ZL = 1 << zl_log2, QB = 256 >> zl_log2;
   const int nq = Ng >> 2;
@@ -618,7 +627,12 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // the 4-B scatters of wgrad_reduce_kernel dominated.
 __global__ void __launch_bounds__(256) wgrad_reduce_tc_kernel(const float* __restrict__ slab, int splits,
                                                               int zl_log2, int K, int C, int RS,
-                                                              float* __restrict__ dw) {
+                                                              float* __restrict__ dw, int nred, bn::BnFinDev fin) {
+  if ((int)blockIdx.x >= nred) {  // a riding BatchNorm backward finalize (see wgrad_reduce_kernel)
+    bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, blockIdx.x - nred, fin.gamma, fin.mean, fin.invstd,
+                                 fin.dgamma, fin.dbeta, fin.coef);
+    return;
+  }
   __shared__ f32x4 part[256];
   __shared__ float outb[64 * 16];
   const int ZL = 1 << zl_log2;
@@ -1002,18 +1016,24 @@ int reduce_zl_log2(int splits, int cap = 16) {
 
 // fixed-order split-K sum of the weight-gradient slabs into torch's [K][C][R][S]
 int launch_wgrad_reduce(const float* slab, int splits, int K, int Ng, int C, int R, int S, int Ci, int im2col,
-                        float* dw, hipStream_t st) {
+                        float* dw, hipStream_t st, const bn::BnFinDev* fin = nullptr) {
   const int RS = R * S;
+  bn::BnFinDev f = {};
+  if (fin) f = *fin;
+  const int nfin = fin ? fin->C : 0;
   if (!im2col && Ci == C && C % 64 == 0 && RS <= 16 && splits <= 16) {
     const int zlg = reduce_zl_log2(splits, 256 / (RS * 16));
-    hipLaunchKernelGGL(wgrad_reduce_tc_kernel, dim3(K * (C / 64)), dim3(256), 0, st, slab, splits, zlg, K, C, RS, dw);
+    const int nred = K * (C / 64);
+    hipLaunchKernelGGL(wgrad_reduce_tc_kernel, dim3(nred + nfin), dim3(256), 0, st, slab, splits, zlg, K, C, RS, dw,
+                       nred, f);
     SQR_HIP_LAUNCH_CHECK("wgrad_reduce_tc_kernel");
     return 0;
   }
   const int total = K * (Ng / 4);
   const int zlg = reduce_zl_log2(splits);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + (256 >> zlg) - 1) / (256 >> zlg)), dim3(256), 0, st, slab,
-                     splits, zlg, K, Ng, C, R, S, Ci, im2col, dw);
+  const int nred = (total + (256 >> zlg) - 1) / (256 >> zlg);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nred + nfin), dim3(256), 0, st, slab, splits, zlg, K, Ng, C, R, S, Ci,
+                     im2col, dw, nred, f);
   SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
   return 0;
 }
@@ -1298,7 +1318,8 @@ static int bwd_data_gemm(const void* dy, const void* w_crsk, void* dx, const sqr
 }
 
 static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, float* dw_kcrs,
-                           const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
+                           const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream,
+                           const bn::BnFinDev* fin = nullptr) {
   Shape sh;
   int rc = check_desc(d, &sh);
   if (rc) return rc;
@@ -1334,7 +1355,7 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
     const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
     rc = conv3w_launch(d->dtype, x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
     if (rc == 0) {
-      rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st);
+      rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st, fin);
       if (rc) return rc;
       return 0;
     }
@@ -1355,13 +1376,33 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   else SQR_DISPATCH16(d->dtype, T, rc = launch_tn<T>(a, p, st));
   if (rc) return rc;
   return launch_wgrad_reduce((const float*)ws, p.splits, d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C,
-                             (int)sh.im2col, dw_kcrs, st);
+                             (int)sh.im2col, dw_kcrs, st, fin);
   return 0;
 }
 
 extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                                      void* workspace, size_t workspace_bytes, void* stream) {
   return bwd_weight_impl(x, nullptr, dy, dw_kcrs, d, workspace, workspace_bytes, stream);
+}
+
+extern "C" int sqr_conv2d_bwd_weight_bnfin(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                                           const sqr_bn_bwd_fin* fin, void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+  SQR_CHECK_ARG(fin && fin->stats && fin->stats_rows > 0 && fin->C > 0 && fin->M > 0 && fin->M < (1ll << 31) &&
+                    fin->save_mean && fin->save_invstd && fin->coef,
+                "conv2d_bwd_weight_bnfin: bad BatchNorm finalize job");
+  bn::BnFinDev f;
+  f.part = fin->stats;
+  f.nblk = fin->stats_rows;
+  f.M = (int)fin->M;
+  f.C = fin->C;
+  f.gamma = fin->gamma;
+  f.mean = fin->save_mean;
+  f.invstd = fin->save_invstd;
+  f.dgamma = fin->dgamma;
+  f.dbeta = fin->dbeta;
+  f.coef = fin->coef;
+  return bwd_weight_impl(x, nullptr, dy, dw_kcrs, d, workspace, workspace_bytes, stream, &f);
 }
 
 extern "C" int sqr_conv2d_bwd_weight_col(const void* col, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,

@@ -34,6 +34,12 @@ class SqrBnOperand(ctypes.Structure):
                 ("save_mean", c_void_p), ("save_invstd", c_void_p)]
 
 
+class SqrBnBwdFin(ctypes.Structure):
+    _fields_ = [("stats", c_void_p), ("stats_rows", c_int), ("M", ctypes.c_longlong), ("C", c_int),
+                ("gamma", c_void_p), ("save_mean", c_void_p), ("save_invstd", c_void_p), ("dgamma", c_void_p),
+                ("dbeta", c_void_p), ("coef", c_void_p)]
+
+
 class SqrTailDesc(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("B", "P", "C0", "F1", "F2", "dtype")] + \
         [("w0", c_void_p), ("b0", c_void_p), ("w1", c_void_p), ("b1", c_void_p),
@@ -90,6 +96,9 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                       c_size_t, c_void_p]),
+    "sqr_conv2d_bwd_weight_bnfin": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),
+                                            ctypes.POINTER(SqrBnBwdFin), c_void_p, c_size_t, c_void_p]),
+    "sqr_bn_bwd_apply": (c_int, [c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sqr_conv2d_bwd_weight_col": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                           c_size_t, c_void_p]),
     "sqr_bn_workspace_bytes": (c_size_t, [ctypes.c_longlong, c_int]),

@@ -68,7 +68,8 @@ class BNActFn(torch.autograd.Function):
         # sqr.conv.BnBackwardLink: the consuming conv's backward-data computes this BN's reduction
         ctx.link = link if (training and relu and residual is None and mask is not None) else None
         if ctx.link is not None:
-            ctx.link.x, ctx.link.mask, ctx.link.mean = x, mask, mean
+            ctx.link.x, ctx.link.mask, ctx.link.mean, ctx.link.invstd = x, mask, mean, invstd
+            ctx.link.gamma, ctx.link.pids = weight, (id(weight), id(bias))
         ctx.pids = (id(weight), id(bias))
         if training:
             ctx.save_for_backward(x, mask, weight, mean, invstd)
@@ -100,7 +101,12 @@ class BNActFn(torch.autograd.Function):
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         got = ctx.link.take(dy) if ctx.link is not None else None
         if got is not None:  # the consuming conv's backward-data already masked g and reduced it
-            g, st = got
+            g, st, coef, dg, db = got
+            if coef is not None:  # ... and its weight-gradient launch finalized this BatchNorm
+                check(lib().sqr_bn_bwd_apply(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(coef), ptr(dx),
+                                             stream_ptr(x.device)), "sqr_bn_bwd_apply")
+                gradbuf.written(ctx.pids)
+                return dx, dg, db, None, None, None, None, None, None, None, None, None, None
             check(lib().sqr_bn_bwd_stats(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(st), st.shape[0],
                                          ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                          stream_ptr(x.device)), "sqr_bn_bwd_stats")

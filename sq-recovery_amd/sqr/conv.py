@@ -8,6 +8,8 @@ torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
 Compute dtype: bfloat16 / float16 when the input has that dtype or CUDA autocast is on with it,
 else float32 (exact-f32 MFMA: the parity mode).
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -27,6 +29,10 @@ _CL = torch.channels_last
 #   clock:  rows of an int64 device tensor [n, 2] receiving the kernel's own wall-clock span
 #           (sqr_probe_arm_clock; works inside replayed graphs: the slot pointer is a kernel argument).
 _probe = {"key": None, "events": [], "clock": None, "nclock": 0}
+
+# ablation switch: SQR_BN_RIDE=0 runs a linked BatchNorm's backward finalize as its own launch
+# instead of as extra workgroups of the conv's weight-gradient reduction
+_RIDE = os.environ.get("SQR_BN_RIDE", "1") != "0"
 
 
 def set_probe(phase, N, C, H, K, R, stride, clock=None):
@@ -214,9 +220,10 @@ def conv2d_bwd_data(gy, w_crsk, d):
     return dx
 
 
-def conv2d_bwd_weight(x, gy, d, col=None, wid=None):
+def conv2d_bwd_weight(x, gy, d, col=None, wid=None, fin=None):
     """dW (fp32, [K,C,R,S]); for C<8 convs pass the forward's workspace as `col` to skip im2col;
-    `wid` = id of the weight parameter (its sqr.gradbuf slot, if any, receives dW)."""
+    `wid` = id of the weight parameter (its sqr.gradbuf slot, if any, receives dW); `fin`: a
+    sqr_bn_bwd_fin job finalized by the same launch (sqr_conv2d_bwd_weight_bnfin)."""
     import ctypes
     dw = gradbuf.out(wid, (d.K, d.C, d.R, d.S), gy.device)
     L = lib()
@@ -225,7 +232,10 @@ def conv2d_bwd_weight(x, gy, d, col=None, wid=None):
         n -= L.sqr_conv2d_workspace_bytes(ctypes.byref(d), 0)
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=gy.device)
     with _Probe("wgrad", d):
-        if col is not None:
+        if fin is not None and col is None:
+            rc = L.sqr_conv2d_bwd_weight_bnfin(ptr(x), ptr(gy), ptr(dw), ctypes.byref(d), ctypes.byref(fin), ptr(ws),
+                                               n, stream_ptr(gy.device))
+        elif col is not None:
             rc = L.sqr_conv2d_bwd_weight_col(ptr(col), ptr(gy), ptr(dw), ctypes.byref(d), ptr(ws), n,
                                              stream_ptr(gy.device))
         else:
@@ -274,10 +284,11 @@ class BnBackwardLink:
     consumer in a BasicBlock), otherwise it runs its own reduction (masking an already-masked g is
     harmless)."""
 
-    __slots__ = ("x", "mask", "mean", "g", "stats")
+    __slots__ = ("x", "mask", "mean", "invstd", "gamma", "pids", "g", "stats", "coef", "dgamma", "dbeta")
 
     def __init__(self):
-        self.x = self.mask = self.mean = self.g = self.stats = None
+        self.x = self.mask = self.mean = self.invstd = self.gamma = self.pids = None
+        self.g = self.stats = self.coef = self.dgamma = self.dbeta = None
 
     @staticmethod
     def make(x, bn):
@@ -290,12 +301,29 @@ class BnBackwardLink:
         return self.x is not None and self.mask is not None and self.mean is not None
 
     def take(self, dy):
-        """(g, stats) if dy is the g this link's conv produced, else None; clears the link."""
-        g, st = self.g, self.stats
-        self.g = self.stats = None
-        if g is None or st is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
+        """(g, stats, coef, dgamma, dbeta) if dy is the g this link's conv produced, else None (coef
+        etc. are None unless the conv's weight-gradient launch also finalized the BatchNorm);
+        clears the link."""
+        got = (self.g, self.stats, self.coef, self.dgamma, self.dbeta)
+        self.g = self.stats = self.coef = self.dgamma = self.dbeta = None
+        g = got[0]
+        if g is None or got[1] is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
             return None
-        return g, st
+        return got
+
+    def fin_job(self, C, device):
+        """The sqr_bn_bwd_fin job of this BatchNorm (outputs allocated here, kept on the link)."""
+        from ._lib import SqrBnBwdFin
+        self.coef = torch.empty(3 * C, dtype=torch.float32, device=device)
+        self.dgamma = gradbuf.out(self.pids[0], (C,), device)
+        self.dbeta = gradbuf.out(self.pids[1], (C,), device)
+        N, _, H, W = self.x.shape
+        f = SqrBnBwdFin()
+        f.stats, f.stats_rows, f.M, f.C = self.stats.data_ptr(), self.stats.shape[0], N * H * W, C
+        f.gamma = self.gamma.data_ptr() if self.gamma is not None else None
+        f.save_mean, f.save_invstd = self.mean.data_ptr(), self.invstd.data_ptr()
+        f.dgamma, f.dbeta, f.coef = self.dgamma.data_ptr(), self.dbeta.data_ptr(), self.coef.data_ptr()
+        return f
 
 
 class ResidualJoin:
@@ -414,7 +442,12 @@ class Conv2dFn(torch.autograd.Function):
             if ctx.join is not None and ctx.role == "dep":
                 dx = ctx.join.deposit(dx)
         if ctx.needs_input_grad[1]:
-            dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid)
+            fin = None
+            link = ctx.bnb
+            if _RIDE and link is not None and link.stats is not None and link.g is not None and col is None \
+                    and link.pids is not None:
+                fin = link.fin_job(d.C, g.device)  # the linked BatchNorm's finalize rides this launch
+            dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid, fin)
             gradbuf.written((ctx.wid,))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
