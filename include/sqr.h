@@ -199,8 +199,30 @@ typedef struct sqr_bn_bwd_fin {
   float* dbeta;             /* nullable */
   float* coef;              /* out, 3*C floats */
 } sqr_bn_bwd_fin;
-int sqr_conv2d_bwd_weight_bnfin(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
-                                const sqr_bn_bwd_fin* fin, void* workspace, size_t workspace_bytes, void* stream);
+/* A BatchNorm backward reduction riding along a weight-gradient launch: dy is the gradient this
+ * conv's backward-data just wrote for the BatchNorm(+ReLU) output that feeds it (a BasicBlock's
+ * input: the previous block's bn2 output, kind 1, or its bn2 + downsample-bn output, kind 2);
+ * part receives (sum g, sum g*(x_a - mean_a)[, sum g*(x_b - mean_b)]) per block, g = dy*mask,
+ * for sqr_bn_bwd_part / sqr_bn_add_bwd_part.  part must hold sqr_bn_bwd_red_doubles(M, C, kind). */
+typedef struct sqr_bn_bwd_red {
+  int kind;
+  const void* dy;
+  const uint8_t* relu_mask;
+  const void* x_a;
+  const float* mean_a;
+  const void* x_b;          /* kind 2 */
+  const float* mean_b;      /* kind 2 */
+  long long M;
+  int C;
+  double* part;             /* out */
+  int* part_rows;           /* out (host memory) */
+} sqr_bn_bwd_red;
+size_t sqr_bn_bwd_red_doubles(long long M, int C, int kind);
+/* the weight gradient with either job (or both, or neither: then = sqr_conv2d_bwd_weight) riding
+ * along its split-K reduction launch */
+int sqr_conv2d_bwd_weight_bn(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                             const sqr_bn_bwd_fin* fin, const sqr_bn_bwd_red* red, void* workspace,
+                             size_t workspace_bytes, void* stream);
 /* C<8 (im2col) convs only: the same from the im2col matrix the forward left at the start of its
  * workspace (sqr_conv2d_workspace_bytes(d,0) bytes), skipping the re-gather; this call's own
  * workspace needs sqr_conv2d_workspace_bytes(d,2) - sqr_conv2d_workspace_bytes(d,0) bytes. */
@@ -239,6 +261,11 @@ int sqr_bn_bwd_stats(const void* g, const void* x, long long M, int C, int dtype
 /* dx = k1*g + k3*x + k2 from finalized coefficients (sqr_conv2d_bwd_weight_bnfin's coef) */
 int sqr_bn_bwd_apply(const void* g, const void* x, long long M, int C, int dtype, const float* coef, void* dx,
                      void* stream);
+/* sqr_bn_bwd from riding-reduction partials (sqr_conv2d_bwd_weight_bn's red job, kind 1) */
+int sqr_bn_bwd_part(const void* dy, const uint8_t* relu_mask, const void* x, long long M, int C, int dtype,
+                    const double* part, int rows, const float* gamma, const float* save_mean,
+                    const float* save_invstd, void* dx, void* dres, float* dgamma, float* dbeta, void* workspace,
+                    size_t workspace_bytes, void* stream);
 
 /* Two-branch BatchNorm: y = act(bn_a(a.x) + bn_b(b.x)) — torchvision BasicBlock with a downsample,
  * relu(bn2(conv2(.)) + bn_ds(conv_ds(x))) (torch/models.py:181).  One apply pass reads both conv
@@ -264,6 +291,11 @@ int sqr_bn_add_fwd(const sqr_bn_operand* a, const sqr_bn_operand* b, long long M
 int sqr_bn_add_bwd(const sqr_bn_operand* a, const sqr_bn_operand* b, const void* dy, const uint8_t* relu_mask,
                    long long M, int C, int dtype, void* dx_a, void* dx_b, float* dgamma_a, float* dbeta_a,
                    float* dgamma_b, float* dbeta_b, void* workspace, size_t workspace_bytes, void* stream);
+/* sqr_bn_add_bwd from riding-reduction partials (kind 2); workspace >= 6*C floats */
+int sqr_bn_add_bwd_part(const sqr_bn_operand* a, const sqr_bn_operand* b, const void* dy, const uint8_t* relu_mask,
+                        long long M, int C, int dtype, const double* part, int rows, void* dx_a, void* dx_b,
+                        float* dgamma_a, float* dbeta_a, float* dgamma_b, float* dbeta_b, void* workspace,
+                        size_t workspace_bytes, void* stream);
 
 /* resnet stem: y = maxpool3x3/s2/p1(relu(bn(x))), x [N][H][W][C] NHWC; argmax [N][Ho][Wo][C] uint8
  * = window tap (dh*3+dw) of the first maximum (torch's tie rule), written when training. */

@@ -7,6 +7,220 @@
 namespace sqr {
 namespace bn {
 
+typedef __bf16 bf16;
+typedef _Float16 f16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 8 consecutive channels as floats
+template <typename T> struct V8;
+template <> struct V8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float* v) {
+    const u32x4 u = *(const u32x4*)p;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* v) {
+    typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+    *(bf16x8*)p = o;
+  }
+};
+template <> struct V8<f16> {
+  static __device__ __forceinline__ void load(const f16* p, float* v) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    const f16x8 u = *(const f16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)u[i];
+  }
+  static __device__ __forceinline__ void store(f16* p, const float* v) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    f16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (f16)v[i];
+    *(f16x8*)p = o;
+  }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float* v) {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[4 + i] = b[i];
+    }
+  }
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+};
+
+__device__ __forceinline__ void load8f(const float* p, float* v) { V8<float>::load(p, v); }
+
+// block geometry for the reductions: V = C/8 channel vectors per pixel, rows = 256 / V
+// partial layout: part[blk][2][C] doubles (sum a, sum b).  8 pixels per iteration per thread so
+// that 8 (16 in the backward) independent 16-B loads are in flight (the loop is latency-bound).
+// (block-level bodies: run by the BatchNorm kernels and, riding along, by sqr_conv.hip's
+// weight-gradient reduction launches)
+template <typename T, int MODE>
+// MODE 0: a = x, b = x^2                                  (forward statistics)
+// MODE 1: g = dy*[relu bit]; a = g, b = g*(x - mean)     (backward; mask = NULL: no ReLU)
+__device__ __forceinline__ void reduce_block(const T* __restrict__ x, const T* __restrict__ dy,
+                                             const uint8_t* __restrict__ mask, const float* __restrict__ mean, int M,
+                                             int C, int chunk, double* __restrict__ part, int blk,
+                                             double* red /* LDS [rows][V][16] */) {
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x;
+  const int row = tid / V, v = tid - row * V;
+  double sa[8], sb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sa[i] = sb[i] = 0.0;
+  float mu[8];
+  if (MODE == 1) load8f(mean + v * 8, mu);
+  const int p0 = blk * chunk, p1 = min(p0 + chunk, M);
+  constexpr int U = 8;
+  for (int pb = p0 + row; pb < p1; pb += U * rows) {
+    float xv[U][8], g[U][8];
+    // branch-free loads (rows past the chunk re-read its last pixel and are masked out below):
+    // all U loads stay in flight together
+    uint32_t mbits[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = min(pb + u * rows, p1 - 1);
+      const size_t off = (size_t)p * C + v * 8;
+      V8<T>::load(x + off, xv[u]);
+      if (MODE == 1) {
+        V8<T>::load(dy + off, g[u]);
+        mbits[u] = mask ? (uint32_t)mask[off >> 3] : 0xffu;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool in = pb + u * rows < p1;
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[u][i] = in ? xv[u][i] : 0.f;
+      } else {
+        const uint32_t mb = in ? mbits[u] : 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[u][i] = (mb >> i) & 1 ? g[u][i] : 0.f;
+      }
+    }
+    // the U pixels of this step in f32 (8 terms), the running sums in f64: one f64 add per
+    // channel and statistic per step instead of per element (the f64 VALU work was the bound)
+    float fa[8], fb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = fb[i] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (MODE == 0) {
+          fa[i] += xv[u][i];
+          fb[i] = fmaf(xv[u][i], xv[u][i], fb[i]);
+        } else {
+          fa[i] += g[u][i];
+          fb[i] = fmaf(g[u][i], xv[u][i] - mu[i], fb[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sa[i] += (double)fa[i];
+      sb[i] += (double)fb[i];
+    }
+  }
+  double* dst = red + ((size_t)row * V + v) * 16;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dst[i] = sa[i];
+    dst[8 + i] = sb[i];
+  }
+  __syncthreads();
+  // fixed-order sum over the rows, one thread per (channel vector, statistic, lane element)
+  double* out = part + (size_t)blk * 2 * C;
+  for (int t = tid; t < V * 16; t += 256) {
+    const int vv = t >> 4, i = t & 15;
+    double acc = 0.0;
+    for (int r = 0; r < rows; ++r) acc += red[((size_t)r * V + vv) * 16 + i];
+    out[(i >> 3) * C + vv * 8 + (i & 7)] = acc;
+  }
+}
+
+// per-block f64 partials [blk][3][C]: sum g, sum g*(xa - mean_a), sum g*(xb - mean_b), g = dy*[mask]
+template <typename T>
+__device__ __forceinline__ void reduce2_block(const T* __restrict__ xa, const T* __restrict__ xb,
+                                              const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                              const float* __restrict__ mean_a, const float* __restrict__ mean_b,
+                                              int M, int C, int chunk, double* __restrict__ part, int blk,
+                                              double* red /* LDS [rows][V][24] */) {
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x;
+  const int row = tid / V, v = tid - row * V;
+  double s0[8], s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0[i] = s1[i] = s2[i] = 0.0;
+  float mua[8], mub[8];
+  load8f(mean_a + v * 8, mua);
+  load8f(mean_b + v * 8, mub);
+  const int p0 = blk * chunk, p1 = min(p0 + chunk, M);
+  constexpr int U = 4;
+  for (int pb = p0 + row; pb < p1; pb += U * rows) {
+    float a[U][8], b[U][8], g[U][8];
+    uint32_t mbits[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = min(pb + u * rows, p1 - 1);
+      const size_t off = (size_t)p * C + v * 8;
+      V8<T>::load(xa + off, a[u]);
+      V8<T>::load(xb + off, b[u]);
+      V8<T>::load(dy + off, g[u]);
+      mbits[u] = mask ? (uint32_t)mask[off >> 3] : 0xffu;
+    }
+    float f0[8], f1[8], f2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f0[i] = f1[i] = f2[i] = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t mb = pb + u * rows < p1 ? mbits[u] : 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float gg = (mb >> i) & 1 ? g[u][i] : 0.f;
+        f0[i] += gg;
+        f1[i] = fmaf(gg, a[u][i] - mua[i], f1[i]);
+        f2[i] = fmaf(gg, b[u][i] - mub[i], f2[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s0[i] += (double)f0[i];
+      s1[i] += (double)f1[i];
+      s2[i] += (double)f2[i];
+    }
+  }
+  double* dst = red + ((size_t)row * V + v) * 24;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    dst[i] = s0[i];
+    dst[8 + i] = s1[i];
+    dst[16 + i] = s2[i];
+  }
+  __syncthreads();
+  double* out = part + (size_t)blk * 3 * C;
+  for (int t = tid; t < V * 24; t += 256) {
+    const int vv = t / 24, i = t - vv * 24;
+    double acc = 0.0;
+    for (int r = 0; r < rows; ++r) acc += red[((size_t)r * V + vv) * 24 + i];
+    out[(i >> 3) * C + vv * 8 + (i & 7)] = acc;
+  }
+}
+
 // one block per channel: thread t sums partials t, t+256, ... (independent loads in flight), then a
 // fixed xor-tree wave reduction and a fixed-order sum of the 4 waves (deterministic).  Returns
 // true on thread 0 only.
@@ -62,6 +276,39 @@ struct BnFinDev {
   const float *gamma, *mean, *invstd;
   float *dgamma, *dbeta, *coef;
 };
+
+// a BatchNorm backward reduction riding along another launch (its extra workgroups): the sums of
+// sqr_bn_bwd (kind 1: reduce_block<T, 1>) or sqr_bn_add_bwd (kind 2: reduce2_block<T>)
+struct BnRedDev {
+  int kind, dtype;  // kind 0: none
+  const void *xa, *xb, *dy;
+  const uint8_t* mask;
+  const float *mean_a, *mean_b;
+  int M, C, chunk, nblk;
+  double* part;
+};
+
+__device__ __forceinline__ void bn_reduce_ride(const BnRedDev& r, int blk, double* lds) {
+  if (r.kind == 1) {
+    if (r.dtype == SQR_DTYPE_BF16)
+      reduce_block<bf16, 1>((const bf16*)r.xa, (const bf16*)r.dy, r.mask, r.mean_a, r.M, r.C, r.chunk, r.part, blk, lds);
+    else if (r.dtype == SQR_DTYPE_F16)
+      reduce_block<f16, 1>((const f16*)r.xa, (const f16*)r.dy, r.mask, r.mean_a, r.M, r.C, r.chunk, r.part, blk, lds);
+    else
+      reduce_block<float, 1>((const float*)r.xa, (const float*)r.dy, r.mask, r.mean_a, r.M, r.C, r.chunk, r.part, blk,
+                             lds);
+  } else {
+    if (r.dtype == SQR_DTYPE_BF16)
+      reduce2_block<bf16>((const bf16*)r.xa, (const bf16*)r.xb, (const bf16*)r.dy, r.mask, r.mean_a, r.mean_b, r.M, r.C,
+                          r.chunk, r.part, blk, lds);
+    else if (r.dtype == SQR_DTYPE_F16)
+      reduce2_block<f16>((const f16*)r.xa, (const f16*)r.xb, (const f16*)r.dy, r.mask, r.mean_a, r.mean_b, r.M, r.C,
+                         r.chunk, r.part, blk, lds);
+    else
+      reduce2_block<float>((const float*)r.xa, (const float*)r.xb, (const float*)r.dy, r.mask, r.mean_a, r.mean_b, r.M,
+                           r.C, r.chunk, r.part, blk, lds);
+  }
+}
 
 }  // namespace bn
 }  // namespace sqr

@@ -41,6 +41,8 @@ int bn_finalize_partials(const float* part, int rows, long long M, int C, const 
 int bn_mask_reduce(void* g, const void* x, const uint8_t* mask, const float* mean, long long M, int C, int dtype,
                    float* stats, int* stats_rows, hipStream_t st);
 size_t bn_mask_reduce_rows(long long M, int C);
+// geometry of the BatchNorm backward reduction (kind 1: reduce_kernel, 2: reduce2_kernel) over M x C
+void bn_red_geometry(long long M, int C, int kind, int* chunk, int* nblk, size_t* lds_bytes);
 int bn_infer_coef(int C, const float* gamma, const float* beta, const float* rmean, const float* rvar, float eps,
                   float* coef, hipStream_t st);
 

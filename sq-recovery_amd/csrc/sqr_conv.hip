@@ -566,15 +566,23 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 // with 8 independent 16-B loads in flight (the pass is HBM/MALL-bound and needs the bytes in
 // flight), then the ZL partial sums are added in a fixed order through LDS -> deterministic.
 // The permuted writes to torch's KCRS layout are 4-B scatters (the output is small).
-// Workgroups past the reduction's own (blockIdx.x >= nred) finalize a BatchNorm backward instead
-// (fin, one channel each): the BatchNorm whose backward sums this conv's backward-data epilogue
-// produced rides along this launch instead of taking one of its own.
+// Workgroups past the reduction's own (blockIdx.x >= nred) do BatchNorm work instead, riding along
+// this launch instead of taking launches of their own: fin.C workgroups finalize the backward of
+// the BatchNorm whose sums this conv's backward-data epilogue produced (one channel each), then
+// rj.nblk workgroups reduce the backward sums of the BatchNorm whose output gradient this conv's
+// backward-data just wrote (the previous block's bn2 / bn2 + downsample-bn).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int zl_log2,
                                                            int K, int Ng, int C, int R, int S, int Ci, int im2col,
-                                                           float* __restrict__ dw, int nred, bn::BnFinDev fin) {
+                                                           float* __restrict__ dw, int nred, bn::BnFinDev fin,
+                                                           bn::BnRedDev rj) {
+  extern __shared__ double ride_lds[];
   if ((int)blockIdx.x >= nred) {
-    bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, blockIdx.x - nred, fin.gamma, fin.mean, fin.invstd,
-                                 fin.dgamma, fin.dbeta, fin.coef);
+    const int b = blockIdx.x - nred;
+    if (b < fin.C)
+      bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, b, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
+                                   fin.dbeta, fin.coef);
+    else
+      bn::bn_reduce_ride(rj, b - fin.C, ride_lds);
     return;
   }
   __shared__ f32x4 part[256];
@@ -627,10 +635,16 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // the 4-B scatters of wgrad_reduce_kernel dominated.
 __global__ void __launch_bounds__(256) wgrad_reduce_tc_kernel(const float* __restrict__ slab, int splits,
                                                               int zl_log2, int K, int C, int RS,
-                                                              float* __restrict__ dw, int nred, bn::BnFinDev fin) {
-  if ((int)blockIdx.x >= nred) {  // a riding BatchNorm backward finalize (see wgrad_reduce_kernel)
-    bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, blockIdx.x - nred, fin.gamma, fin.mean, fin.invstd,
-                                 fin.dgamma, fin.dbeta, fin.coef);
+                                                              float* __restrict__ dw, int nred, bn::BnFinDev fin,
+                                                              bn::BnRedDev rj) {
+  extern __shared__ double ride_lds[];
+  if ((int)blockIdx.x >= nred) {  // riding BatchNorm work (see wgrad_reduce_kernel)
+    const int b = blockIdx.x - nred;
+    if (b < fin.C)
+      bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, b, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
+                                   fin.dbeta, fin.coef);
+    else
+      bn::bn_reduce_ride(rj, b - fin.C, ride_lds);
     return;
   }
   __shared__ f32x4 part[256];
@@ -1016,24 +1030,28 @@ int reduce_zl_log2(int splits, int cap = 16) {
 
 // fixed-order split-K sum of the weight-gradient slabs into torch's [K][C][R][S]
 int launch_wgrad_reduce(const float* slab, int splits, int K, int Ng, int C, int R, int S, int Ci, int im2col,
-                        float* dw, hipStream_t st, const bn::BnFinDev* fin = nullptr) {
+                        float* dw, hipStream_t st, const bn::BnFinDev* fin = nullptr,
+                        const bn::BnRedDev* red = nullptr, size_t red_lds = 0) {
   const int RS = R * S;
   bn::BnFinDev f = {};
+  bn::BnRedDev r = {};
   if (fin) f = *fin;
-  const int nfin = fin ? fin->C : 0;
+  if (red) r = *red;
+  const int nride = (fin ? fin->C : 0) + (red ? red->nblk : 0);
+  const size_t lds = red ? red_lds : 0;
   if (!im2col && Ci == C && C % 64 == 0 && RS <= 16 && splits <= 16) {
     const int zlg = reduce_zl_log2(splits, 256 / (RS * 16));
     const int nred = K * (C / 64);
-    hipLaunchKernelGGL(wgrad_reduce_tc_kernel, dim3(nred + nfin), dim3(256), 0, st, slab, splits, zlg, K, C, RS, dw,
-                       nred, f);
+    hipLaunchKernelGGL(wgrad_reduce_tc_kernel, dim3(nred + nride), dim3(256), lds, st, slab, splits, zlg, K, C, RS, dw,
+                       nred, f, r);
     SQR_HIP_LAUNCH_CHECK("wgrad_reduce_tc_kernel");
     return 0;
   }
   const int total = K * (Ng / 4);
   const int zlg = reduce_zl_log2(splits);
   const int nred = (total + (256 >> zlg) - 1) / (256 >> zlg);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nred + nfin), dim3(256), 0, st, slab, splits, zlg, K, Ng, C, R, S, Ci,
-                     im2col, dw, nred, f);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nred + nride), dim3(256), lds, st, slab, splits, zlg, K, Ng, C, R, S,
+                     Ci, im2col, dw, nred, f, r);
   SQR_HIP_LAUNCH_CHECK("wgrad_reduce_kernel");
   return 0;
 }
@@ -1319,7 +1337,8 @@ static int bwd_data_gemm(const void* dy, const void* w_crsk, void* dx, const sqr
 
 static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, float* dw_kcrs,
                            const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream,
-                           const bn::BnFinDev* fin = nullptr) {
+                           const bn::BnFinDev* fin = nullptr, const bn::BnRedDev* red = nullptr,
+                           size_t red_lds = 0) {
   Shape sh;
   int rc = check_desc(d, &sh);
   if (rc) return rc;
@@ -1355,7 +1374,8 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
     const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
     rc = conv3w_launch(d->dtype, x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
     if (rc == 0) {
-      rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st, fin);
+      rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st, fin, red,
+                               red_lds);
       if (rc) return rc;
       return 0;
     }
@@ -1376,7 +1396,7 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   else SQR_DISPATCH16(d->dtype, T, rc = launch_tn<T>(a, p, st));
   if (rc) return rc;
   return launch_wgrad_reduce((const float*)ws, p.splits, d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C,
-                             (int)sh.im2col, dw_kcrs, st, fin);
+                             (int)sh.im2col, dw_kcrs, st, fin, red, red_lds);
   return 0;
 }
 
@@ -1385,24 +1405,50 @@ extern "C" int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kc
   return bwd_weight_impl(x, nullptr, dy, dw_kcrs, d, workspace, workspace_bytes, stream);
 }
 
-extern "C" int sqr_conv2d_bwd_weight_bnfin(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
-                                           const sqr_bn_bwd_fin* fin, void* workspace, size_t workspace_bytes,
-                                           void* stream) {
-  SQR_CHECK_ARG(fin && fin->stats && fin->stats_rows > 0 && fin->C > 0 && fin->M > 0 && fin->M < (1ll << 31) &&
-                    fin->save_mean && fin->save_invstd && fin->coef,
-                "conv2d_bwd_weight_bnfin: bad BatchNorm finalize job");
-  bn::BnFinDev f;
-  f.part = fin->stats;
-  f.nblk = fin->stats_rows;
-  f.M = (int)fin->M;
-  f.C = fin->C;
-  f.gamma = fin->gamma;
-  f.mean = fin->save_mean;
-  f.invstd = fin->save_invstd;
-  f.dgamma = fin->dgamma;
-  f.dbeta = fin->dbeta;
-  f.coef = fin->coef;
-  return bwd_weight_impl(x, nullptr, dy, dw_kcrs, d, workspace, workspace_bytes, stream, &f);
+extern "C" int sqr_conv2d_bwd_weight_bn(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
+                                        const sqr_bn_bwd_fin* fin, const sqr_bn_bwd_red* red, void* workspace,
+                                        size_t workspace_bytes, void* stream) {
+  bn::BnFinDev f = {};
+  if (fin) {
+    SQR_CHECK_ARG(fin->stats && fin->stats_rows > 0 && fin->C > 0 && fin->M > 0 && fin->M < (1ll << 31) &&
+                      fin->save_mean && fin->save_invstd && fin->coef,
+                  "conv2d_bwd_weight_bn: bad BatchNorm finalize job");
+    f.part = fin->stats;
+    f.nblk = fin->stats_rows;
+    f.M = (int)fin->M;
+    f.C = fin->C;
+    f.gamma = fin->gamma;
+    f.mean = fin->save_mean;
+    f.invstd = fin->save_invstd;
+    f.dgamma = fin->dgamma;
+    f.dbeta = fin->dbeta;
+    f.coef = fin->coef;
+  }
+  bn::BnRedDev r = {};
+  size_t lds = 0;
+  if (red) {
+    SQR_CHECK_ARG((red->kind == 1 || red->kind == 2) && red->dy && red->relu_mask && red->x_a && red->mean_a &&
+                      (red->kind == 1 || (red->x_b && red->mean_b)) && red->part && red->part_rows,
+                  "conv2d_bwd_weight_bn: bad BatchNorm reduction job");
+    SQR_CHECK_ARG(red->M > 0 && red->M < (1ll << 31) && red->C >= 8 && red->C <= 2048 && red->C % 8 == 0 &&
+                      256 % (red->C / 8) == 0,
+                  "conv2d_bwd_weight_bn: bad reduction shape M=%lld C=%d", red->M, red->C);
+    r.kind = red->kind;
+    r.dtype = d->dtype;
+    r.xa = red->x_a;
+    r.xb = red->x_b;
+    r.dy = red->dy;
+    r.mask = red->relu_mask;
+    r.mean_a = red->mean_a;
+    r.mean_b = red->mean_b;
+    r.M = (int)red->M;
+    r.C = red->C;
+    r.part = red->part;
+    bn_red_geometry(red->M, red->C, red->kind, &r.chunk, &r.nblk, &lds);
+    *red->part_rows = r.nblk;
+  }
+  return bwd_weight_impl(x, nullptr, dy, dw_kcrs, d, workspace, workspace_bytes, stream, fin ? &f : nullptr,
+                         red ? &r : nullptr, lds);
 }
 
 extern "C" int sqr_conv2d_bwd_weight_col(const void* col, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,

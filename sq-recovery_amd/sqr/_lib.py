@@ -40,6 +40,12 @@ class SqrBnBwdFin(ctypes.Structure):
                 ("dbeta", c_void_p), ("coef", c_void_p)]
 
 
+class SqrBnBwdRed(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("dy", c_void_p), ("relu_mask", c_void_p), ("x_a", c_void_p), ("mean_a", c_void_p),
+                ("x_b", c_void_p), ("mean_b", c_void_p), ("M", ctypes.c_longlong), ("C", c_int), ("part", c_void_p),
+                ("part_rows", ctypes.POINTER(c_int))]
+
+
 class SqrTailDesc(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("B", "P", "C0", "F1", "F2", "dtype")] + \
         [("w0", c_void_p), ("b0", c_void_p), ("w1", c_void_p), ("b1", c_void_p),
@@ -96,8 +102,16 @@ SIGNATURES = {
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                       c_size_t, c_void_p]),
-    "sqr_conv2d_bwd_weight_bnfin": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),
-                                            ctypes.POINTER(SqrBnBwdFin), c_void_p, c_size_t, c_void_p]),
+    "sqr_conv2d_bwd_weight_bn": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),
+                                         ctypes.POINTER(SqrBnBwdFin), ctypes.POINTER(SqrBnBwdRed), c_void_p, c_size_t,
+                                         c_void_p]),
+    "sqr_bn_bwd_red_doubles": (c_size_t, [ctypes.c_longlong, c_int, c_int]),
+    "sqr_bn_bwd_part": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_int,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_size_t, c_void_p]),
+    "sqr_bn_add_bwd_part": (c_int, [ctypes.POINTER(SqrBnOperand), ctypes.POINTER(SqrBnOperand), c_void_p, c_void_p,
+                                    ctypes.c_longlong, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_bn_bwd_apply": (c_int, [c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "sqr_conv2d_bwd_weight_col": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                           c_size_t, c_void_p]),

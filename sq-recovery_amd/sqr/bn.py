@@ -36,7 +36,7 @@ def _ws_bytes(M, C):
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps, stats=None,
-                res_join=None, link=None):
+                res_join=None, link=None, out_link=None):
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
@@ -70,6 +70,10 @@ class BNActFn(torch.autograd.Function):
         if ctx.link is not None:
             ctx.link.x, ctx.link.mask, ctx.link.mean, ctx.link.invstd = x, mask, mean, invstd
             ctx.link.gamma, ctx.link.pids = weight, (id(weight), id(bias))
+        # sqr.conv.BnOutLink: the next block's conv1 reduces this BN's backward sums in its launch
+        ctx.out_link = out_link if (training and relu and mask is not None) else None
+        if ctx.out_link is not None:
+            ctx.out_link.x_a, ctx.out_link.mean_a, ctx.out_link.mask = x, mean, mask
         ctx.pids = (id(weight), id(bias))
         if training:
             ctx.save_for_backward(x, mask, weight, mean, invstd)
@@ -92,13 +96,24 @@ class BNActFn(torch.autograd.Function):
             if ctx.res_join is not None:
                 dres = ctx.res_join.deposit(dres)
             return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None, None, \
-                None
+                None, None
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
         dgamma = gradbuf.out(ctx.pids[0], (C,), x.device)
         dbeta = gradbuf.out(ctx.pids[1], (C,), x.device)
         n = _ws_bytes(M, C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        part = ctx.out_link.take(dy) if ctx.out_link is not None else None
+        if part is not None:  # the next block's conv1 already reduced (dy, mask, x) in its launch
+            check(lib().sqr_bn_bwd_part(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(part[0]), part[1],
+                                        ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta),
+                                        ptr(ws), n, stream_ptr(x.device)), "sqr_bn_bwd_part")
+            gradbuf.written(ctx.pids)
+            if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
+                dres = dy
+            if ctx.res_join is not None:
+                dres = ctx.res_join.deposit(dres)
+            return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
         got = ctx.link.take(dy) if ctx.link is not None else None
         if got is not None:  # the consuming conv's backward-data already masked g and reduced it
             g, st, coef, dg, db = got
@@ -106,12 +121,12 @@ class BNActFn(torch.autograd.Function):
                 check(lib().sqr_bn_bwd_apply(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(coef), ptr(dx),
                                              stream_ptr(x.device)), "sqr_bn_bwd_apply")
                 gradbuf.written(ctx.pids)
-                return dx, dg, db, None, None, None, None, None, None, None, None, None, None
+                return dx, dg, db, None, None, None, None, None, None, None, None, None, None, None
             check(lib().sqr_bn_bwd_stats(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(st), st.shape[0],
                                          ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                          stream_ptr(x.device)), "sqr_bn_bwd_stats")
             gradbuf.written(ctx.pids)
-            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
+            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
         check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
@@ -120,7 +135,7 @@ class BNActFn(torch.autograd.Function):
             dres = dy
         if ctx.res_join is not None:
             dres = ctx.res_join.deposit(dres)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
 
 
 def count_batches(bns):
@@ -146,7 +161,7 @@ def _check_stats(stats, x):
     return stats
 
 
-def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=None):
+def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=None, out_link=None):
     """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics.
     x may be a (y, partials) pair from a stats-producing conv: training mode then takes the batch
     statistics from the partials instead of reducing over y.  res_join: the residual input's
@@ -160,7 +175,7 @@ def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=N
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
-                         _check_stats(stats, x), res_join if residual is not None else None, link)
+                         _check_stats(stats, x), res_join if residual is not None else None, link, out_link)
 
 
 def _operand(x, stats, weight, bias, rmean, rvar, momentum, eps, mean, invstd):
@@ -184,7 +199,7 @@ class BNAddActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xa, wa, ba, rma, rva, xb, wb, bb, rmb, rvb, relu, training, mom_a, mom_b, eps_a, eps_b,
-                stats_a, stats_b):
+                stats_a, stats_b, out_link=None):
         xa = xa.contiguous(memory_format=_CL)
         xb = xb.to(xa.dtype).contiguous(memory_format=_CL)
         N, C, H, W = xa.shape
@@ -203,6 +218,10 @@ class BNAddActFn(torch.autograd.Function):
         ctx.training = training
         ctx.eps = (eps_a, eps_b)
         ctx.pids = (id(wa), id(ba), id(wb), id(bb))
+        ctx.out_link = out_link if (training and mask is not None) else None
+        if ctx.out_link is not None:  # sqr.conv.BnOutLink (kind 2)
+            ctx.out_link.x_a, ctx.out_link.mean_a, ctx.out_link.x_b, ctx.out_link.mean_b = xa, ma, xb, mb
+            ctx.out_link.mask = mask
         if training:
             ctx.save_for_backward(xa, xb, mask, wa, wb, ma, ia, mb, ib)
         else:
@@ -225,7 +244,7 @@ class BNAddActFn(torch.autograd.Function):
                 out.append(((g * (w * invstd).view(1, C, 1, 1)).to(x.dtype), (g * xhat).sum((0, 2, 3)),
                             g.sum((0, 2, 3))))
             (dxa, dga, dba), (dxb, dgb, dbb) = out
-            return dxa, dga, dba, None, None, dxb, dgb, dbb, None, None, None, None, None, None, None, None, None, None
+            return (dxa, dga, dba, None, None, dxb, dgb, dbb) + (None,) * 11
         dxa = torch.empty_like(xa, memory_format=_CL)
         dxb = torch.empty_like(xb, memory_format=_CL)
         dga = gradbuf.out(ctx.pids[0], (C,), xa.device)
@@ -237,14 +256,20 @@ class BNAddActFn(torch.autograd.Function):
         L = lib()
         n = L.sqr_bn_add_workspace_bytes(ctypes.c_longlong(M), C)
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=xa.device)
-        check(L.sqr_bn_add_bwd(ctypes.byref(oa), ctypes.byref(ob), ptr(dy), ptr(ym), ctypes.c_longlong(M), C, _dt(xa),
-                               ptr(dxa), ptr(dxb), ptr(dga), ptr(dba), ptr(dgb), ptr(dbb), ptr(ws), n,
-                               stream_ptr(xa.device)), "sqr_bn_add_bwd")
+        part = ctx.out_link.take(dy) if ctx.out_link is not None else None
+        if part is not None:  # the next block's conv1 already reduced (dy, mask, xa, xb) in its launch
+            check(L.sqr_bn_add_bwd_part(ctypes.byref(oa), ctypes.byref(ob), ptr(dy), ptr(ym), ctypes.c_longlong(M), C,
+                                        _dt(xa), ptr(part[0]), part[1], ptr(dxa), ptr(dxb), ptr(dga), ptr(dba),
+                                        ptr(dgb), ptr(dbb), ptr(ws), n, stream_ptr(xa.device)), "sqr_bn_add_bwd_part")
+        else:
+            check(L.sqr_bn_add_bwd(ctypes.byref(oa), ctypes.byref(ob), ptr(dy), ptr(ym), ctypes.c_longlong(M), C,
+                                   _dt(xa), ptr(dxa), ptr(dxb), ptr(dga), ptr(dba), ptr(dgb), ptr(dbb), ptr(ws), n,
+                                   stream_ptr(xa.device)), "sqr_bn_add_bwd")
         gradbuf.written(ctx.pids)
-        return dxa, dga, dba, None, None, dxb, dgb, dbb, None, None, None, None, None, None, None, None, None, None
+        return (dxa, dga, dba, None, None, dxb, dgb, dbb) + (None,) * 11
 
 
-def bn_add_act(xa, bn_a, xb, bn_b, relu=True, counted=False):
+def bn_add_act(xa, bn_a, xb, bn_b, relu=True, counted=False, out_link=None):
     """relu?(bn_a(xa) + bn_b(xb)) (two nn.BatchNorm2d, same channel count).  xa / xb may be
     (y, partials) pairs from stats-producing convs; training mode needs both partials."""
     xa, sa = _split(xa)
@@ -266,7 +291,7 @@ def bn_add_act(xa, bn_a, xb, bn_b, relu=True, counted=False):
     (rma, rva, moma, epsa), (rmb, rvb, momb, epsb) = args
     return BNAddActFn.apply(xa, bn_a.weight, bn_a.bias, rma, rva, xb, bn_b.weight, bn_b.bias, rmb, rvb, bool(relu),
                             bool(ta), moma, momb, epsa, epsb, _check_stats(sa, xa) if ta else None,
-                            _check_stats(sb, xb) if ta else None)
+                            _check_stats(sb, xb) if ta else None, out_link)
 
 
 class StemFn(torch.autograd.Function):

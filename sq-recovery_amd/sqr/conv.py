@@ -220,10 +220,10 @@ def conv2d_bwd_data(gy, w_crsk, d):
     return dx
 
 
-def conv2d_bwd_weight(x, gy, d, col=None, wid=None, fin=None):
+def conv2d_bwd_weight(x, gy, d, col=None, wid=None, fin=None, red=None):
     """dW (fp32, [K,C,R,S]); for C<8 convs pass the forward's workspace as `col` to skip im2col;
-    `wid` = id of the weight parameter (its sqr.gradbuf slot, if any, receives dW); `fin`: a
-    sqr_bn_bwd_fin job finalized by the same launch (sqr_conv2d_bwd_weight_bnfin)."""
+    `wid` = id of the weight parameter (its sqr.gradbuf slot, if any, receives dW); `fin` / `red`:
+    sqr_bn_bwd_fin / sqr_bn_bwd_red jobs riding the same launch (sqr_conv2d_bwd_weight_bn)."""
     import ctypes
     dw = gradbuf.out(wid, (d.K, d.C, d.R, d.S), gy.device)
     L = lib()
@@ -232,9 +232,11 @@ def conv2d_bwd_weight(x, gy, d, col=None, wid=None, fin=None):
         n -= L.sqr_conv2d_workspace_bytes(ctypes.byref(d), 0)
     ws = torch.empty(max(n, 16), dtype=torch.uint8, device=gy.device)
     with _Probe("wgrad", d):
-        if fin is not None and col is None:
-            rc = L.sqr_conv2d_bwd_weight_bnfin(ptr(x), ptr(gy), ptr(dw), ctypes.byref(d), ctypes.byref(fin), ptr(ws),
-                                               n, stream_ptr(gy.device))
+        if (fin is not None or red is not None) and col is None:
+            rc = L.sqr_conv2d_bwd_weight_bn(ptr(x), ptr(gy), ptr(dw), ctypes.byref(d),
+                                            ctypes.byref(fin) if fin is not None else None,
+                                            ctypes.byref(red) if red is not None else None, ptr(ws), n,
+                                            stream_ptr(gy.device))
         elif col is not None:
             rc = L.sqr_conv2d_bwd_weight_col(ptr(col), ptr(gy), ptr(dw), ctypes.byref(d), ptr(ws), n,
                                              stream_ptr(gy.device))
@@ -326,6 +328,50 @@ class BnBackwardLink:
         return f
 
 
+class BnOutLink:
+    """A BasicBlock's output BatchNorm (bn2 + residual + ReLU, or bn2 + downsample-bn + ReLU) and the
+    next block's conv1: that conv's backward-data writes the gradient of this output (the residual
+    branch's share added in its epilogue, see ResidualJoin), so its weight-gradient launch also runs
+    the BatchNorm's backward reduction over it (sqr_conv2d_bwd_weight_bn's red job); the
+    BatchNorm's backward then only finalizes and applies — if the gradient it receives IS that one."""
+
+    __slots__ = ("kind", "x_a", "mean_a", "x_b", "mean_b", "mask", "g", "part", "rows")
+
+    def __init__(self, kind):
+        self.kind = kind
+        self.x_a = self.mean_a = self.x_b = self.mean_b = self.mask = None
+        self.g = self.part = self.rows = None
+
+    def ready(self):
+        return self.x_a is not None and self.mask is not None and (self.kind == 1 or self.x_b is not None)
+
+    def red_job(self, dx):
+        import ctypes
+        from ._lib import SqrBnBwdRed
+        N, C, H, W = self.x_a.shape
+        M = N * H * W
+        n = lib().sqr_bn_bwd_red_doubles(ctypes.c_longlong(M), C, self.kind)
+        self.part = torch.empty(max(n, 1), dtype=torch.float64, device=dx.device)
+        self.rows = ctypes.c_int()
+        self.g = dx
+        r = SqrBnBwdRed()
+        r.kind, r.dy, r.relu_mask = self.kind, dx.data_ptr(), self.mask.data_ptr()
+        r.x_a, r.mean_a = self.x_a.data_ptr(), self.mean_a.data_ptr()
+        r.x_b = self.x_b.data_ptr() if self.x_b is not None else None
+        r.mean_b = self.mean_b.data_ptr() if self.mean_b is not None else None
+        r.M, r.C, r.part = M, C, self.part.data_ptr()
+        r.part_rows = ctypes.pointer(self.rows)
+        return r
+
+    def take(self, dy):
+        """(part, rows) if dy is the gradient the riding reduction summed, else None; clears."""
+        g, part, rows = self.g, self.part, self.rows
+        self.g = self.part = self.rows = None
+        if g is None or part is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
+            return None
+        return part, rows.value
+
+
 class ResidualJoin:
     """The two gradient contributions of a residual block's input x (torchvision BasicBlock:
     x feeds conv1 AND the identity / downsample branch, torch/models.py:181) summed without a
@@ -379,7 +425,8 @@ def compute_dtype(x):
 
 class Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False, join=None, role=None, bnb=None):
+    def forward(ctx, x, weight, bias, stride, pad, dt, packed, want_stats=False, join=None, role=None, bnb=None,
+                bnr=None):
         # the statistics output is non-differentiable: don't let autograd materialise a zero
         # gradient tensor for it in backward
         ctx.set_materialize_grads(False)
@@ -402,6 +449,7 @@ class Conv2dFn(torch.autograd.Function):
         ctx.d = d
         ctx.join, ctx.role = join, role  # ResidualJoin of x: role "acc" (conv1) / "dep" (downsample)
         ctx.bnb = bnb  # BnBackwardLink of x's BatchNorm (bn1 -> relu -> this conv)
+        ctx.bnr = bnr  # BnOutLink of x's producer (the previous block's output BatchNorm)
         ctx.wid = id(weight)
         ctx.x_dtype = x.dtype
         ctx.has_bias = bias is not None
@@ -417,12 +465,13 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, *_):
         if gy is None:  # grads are not materialised (see forward)
-            return (None,) * 11
+            return (None,) * 12
         xin, crsk, col = ctx.saved_tensors
         d = ctx.d
         dt = _TORCH_DT[d.dtype]
         g = gy.to(dt).contiguous(memory_format=_CL)
         dx = dw = db = None
+        ride_red = None
         if ctx.needs_input_grad[0]:
             if crsk is None:
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
@@ -434,6 +483,7 @@ class Conv2dFn(torch.autograd.Function):
             elif addend is not None and addend.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W) \
                     and addend.is_contiguous(memory_format=_CL):
                 dx = conv2d_bwd_data_acc(g, crsk, d, addend)
+                ride_red = ctx.bnr  # dx is the whole gradient of x: its BatchNorm reduction can ride
             else:
                 dx = conv2d_bwd_data(g, crsk, d)
                 if addend is not None:
@@ -447,21 +497,26 @@ class Conv2dFn(torch.autograd.Function):
             if _RIDE and link is not None and link.stats is not None and link.g is not None and col is None \
                     and link.pids is not None:
                 fin = link.fin_job(d.C, g.device)  # the linked BatchNorm's finalize rides this launch
-            dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid, fin)
+            red = None
+            if _RIDE and ride_red is not None and ride_red.ready() and col is None and dx is not None \
+                    and dx.dtype == ride_red.x_a.dtype and dx.shape == ride_red.x_a.shape:
+                red = ride_red.red_job(dx)
+            dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid, fin, red)
             gradbuf.written((ctx.wid,))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = g.float().sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None, None, None
 
 
-def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False, join=None, role=None, bnb=None):
+def conv2d(x, weight, bias=None, stride=1, padding=0, packed=None, stats=False, join=None, role=None, bnb=None,
+           bnr=None):
     """conv(x); with stats=True returns (y, partials) where partials feed the following
     BatchNorm (sqr.bn.bn_act / stem ``stats=``) so it skips its statistics pass over y
     (partials is None when the conv has a bias)."""
     if not x.is_cuda:
         raise ValueError("sqr conv2d runs on MI355X; got a %s tensor" % x.device)
     return Conv2dFn.apply(x, weight, bias, int(stride), int(padding), compute_dtype(x), packed, bool(stats), join,
-                          role, bnb)
+                          role, bnb, bnr)
 
 
 class Conv2d(nn.Conv2d):
@@ -488,7 +543,7 @@ class Conv2d(nn.Conv2d):
             return super().forward(x)
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x))
 
-    def forward_stats(self, x, bn=None, join=None, role=None, bnb=None):
+    def forward_stats(self, x, bn=None, join=None, role=None, bnb=None, bnr=None):
         """(y, BatchNorm partials of y) — see conv2d(stats=True).  With `bn` given, the partials
         are produced only when that BatchNorm will use batch statistics (else y alone).  join/role:
         a ResidualJoin of x (see there)."""
@@ -496,4 +551,4 @@ class Conv2d(nn.Conv2d):
             return self.forward(x)
         want = bn is None or bn.training or not bn.track_running_stats
         return conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self._cached(x), stats=want,
-                      join=join, role=role, bnb=bnb)
+                      join=join, role=role, bnb=bnb, bnr=bnr)

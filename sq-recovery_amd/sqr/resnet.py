@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from .bn import bn_act, bn_add_act, count_batches, fused_stem, fused_stem_ok, stem
-from .conv import BnBackwardLink, Conv2d, ResidualJoin, compute_dtype, pack_all
+from .conv import BnBackwardLink, BnOutLink, Conv2d, ResidualJoin, compute_dtype, pack_all
 
 
 # ablation switches (A/B timing in one process / on one box; both default on):
@@ -49,8 +49,12 @@ class BasicBlock(nn.Module):
         # epilogue through a ResidualJoin instead of a separate add)
         join = ResidualJoin.make(x) if _JOIN else None
         link = BnBackwardLink.make(x, self.bn1) if _BN_LINK else None
-        out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc"), self.bn1, relu=True, counted=True,
-                     link=link)
+        # x's producer (the previous block's output BatchNorm) may have its backward reduction ride
+        # on conv1's weight-gradient launch (BnOutLink)
+        red_link = getattr(x, "_sqr_outlink", None) if join is not None else None
+        out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc", bnr=red_link), self.bn1, relu=True,
+                     counted=True, link=link)
+        out_link = BnOutLink(2 if self.downsample is not None else 1) if (join is not None and _BN_LINK) else None
         if self.downsample is not None and not _BN_ADD:
             identity = bn_act(self.downsample[0].forward_stats(x, self.downsample[1], join=join, role="dep"),
                               self.downsample[1], relu=False, counted=True)
@@ -60,10 +64,14 @@ class BasicBlock(nn.Module):
             # bn2(conv2) + bn_ds(conv_ds) + ReLU as ONE op: the downsample branch is never normalised
             # into a tensor of its own (sqr_bn_add_*)
             ds = self.downsample[0].forward_stats(x, self.downsample[1], join=join, role="dep")
-            return bn_add_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, ds, self.downsample[1],
-                              relu=True, counted=True)
-        return bn_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, residual=x, relu=True, counted=True,
-                      res_join=join)
+            y = bn_add_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, ds, self.downsample[1],
+                           relu=True, counted=True, out_link=out_link)
+        else:
+            y = bn_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, residual=x, relu=True, counted=True,
+                       res_join=join, out_link=out_link)
+        if out_link is not None:
+            y._sqr_outlink = out_link
+        return y
 
 
 class ResNet18(nn.Module):
