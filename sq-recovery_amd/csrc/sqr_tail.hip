@@ -304,8 +304,13 @@ struct WOut {
 
 // 4 weight rows per block: section 0 = fc.0 rows (act = feat), 1 = fc.2 rows (act = leaky(pre0)),
 // 2 = head rows (act = leaky(pre1)).  dW[r][c] = sum_n d[n][r] act[n][c] in sample order.
+// Samples go 64 at a time: the block's 4 x 64 d values are staged in LDS once, and each thread
+// issues its 64 activation loads together (one memory round trip per chunk instead of one per 8
+// samples: the loop was latency-bound); the sum order is unchanged.
+constexpr int WG_CHUNK = 64;
 __global__ void __launch_bounds__(256) tail_wgrad_kernel(Dev d, const float* __restrict__ save,
                                                          const float* __restrict__ dsave, WOut o) {
+  __shared__ float dsh[WG_CHUNK][4];
   const int b0n = d.F1 / 4, b1n = d.F2 / 4;
   int sec, r0;
   if ((int)blockIdx.x < b0n) {
@@ -322,31 +327,65 @@ __global__ void __launch_bounds__(256) tail_wgrad_kernel(Dev d, const float* __r
   const int aoff = sec == 0 ? 0 : (sec == 1 ? d.C0 : d.C0 + d.F1);        // activation in save
   const int doff = sec == 0 ? 0 : (sec == 1 ? d.F1 : d.F1 + d.F2);        // d in dsave
   const int ldd = d.F1 + d.F2 + NOUT;
-  for (int c = threadIdx.x; c < ncols; c += 256) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int n = 0; n < d.B; ++n) {
-      float a = save[(size_t)n * d.ldsave + aoff + c];
-      if (sec > 0) a = leaky(a);
-      const float* dn = dsave + (size_t)n * ldd + doff + r0;
+  const int ncb = (ncols + 255) / 256;  // column passes (<= MAXF / 256)
+  float acc[MAXF / 256][4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[u] = fmaf(dn[u], a, acc[u]);
+  for (int q = 0; q < MAXF / 256; ++q)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[q][u] = 0.f;
+  float bsum = 0.f;  // thread u < 4: db of row r0 + u
+  for (int n0 = 0; n0 < d.B; n0 += WG_CHUNK) {
+    const int nn = min(WG_CHUNK, d.B - n0);
+    __syncthreads();  // the previous chunk's d values are consumed
+    {
+      const int n = threadIdx.x >> 2, u = threadIdx.x & 3;
+      if (n < nn) dsh[n][u] = dsave[(size_t)(n0 + n) * ldd + doff + r0 + u];
     }
+    __syncthreads();
+    if (threadIdx.x < 4)
+      for (int n = 0; n < nn; ++n) bsum += dsh[n][threadIdx.x];
+#pragma unroll
+    for (int q = 0; q < MAXF / 256; ++q) {
+      const int c = q * 256 + threadIdx.x;
+      if (q >= ncb || c >= ncols) continue;
+      float a[WG_CHUNK];
+#pragma unroll
+      for (int n = 0; n < WG_CHUNK; ++n)
+        a[n] = n < nn ? save[(size_t)(n0 + n) * d.ldsave + aoff + min(c, ncols - 1)] : 0.f;
+      if (nn == WG_CHUNK) {
+#pragma unroll
+        for (int n = 0; n < WG_CHUNK; ++n) {
+          const float an = sec > 0 ? leaky(a[n]) : a[n];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[q][u] = fmaf(dsh[n][u], an, acc[q][u]);
+        }
+      } else {  // a partial last chunk
+        for (int n = 0; n < nn; ++n) {
+          const float an = sec > 0 ? leaky(save[(size_t)(n0 + n) * d.ldsave + aoff + c])
+                                   : save[(size_t)(n0 + n) * d.ldsave + aoff + c];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[q][u] = fmaf(dsh[n][u], an, acc[q][u]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXF / 256; ++q) {
+    const int c = q * 256 + threadIdx.x;
+    if (q >= ncb || c >= ncols) continue;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int r = r0 + u;
-      if (sec == 0) o.dw0[(size_t)r * ncols + c] = acc[u];
-      else if (sec == 1) o.dw1[(size_t)r * ncols + c] = acc[u];
-      else o.dwh[head_of(r)][(size_t)head_row(r) * ncols + c] = acc[u];
+      if (sec == 0) o.dw0[(size_t)r * ncols + c] = acc[q][u];
+      else if (sec == 1) o.dw1[(size_t)r * ncols + c] = acc[q][u];
+      else o.dwh[head_of(r)][(size_t)head_row(r) * ncols + c] = acc[q][u];
     }
   }
   if (threadIdx.x < 4) {
     const int r = r0 + threadIdx.x;
-    float s = 0.f;
-    for (int n = 0; n < d.B; ++n) s += dsave[(size_t)n * ldd + doff + r];
-    if (sec == 0) o.db0[r] = s;
-    else if (sec == 1) o.db1[r] = s;
-    else o.dbh[head_of(r)][head_row(r)] = s;
+    if (sec == 0) o.db0[r] = bsum;
+    else if (sec == 1) o.db1[r] = bsum;
+    else o.dbh[head_of(r)][head_row(r)] = bsum;
   }
 }
 
