@@ -20,6 +20,7 @@
 // buffer descriptor range check (voffset = 0x80000000).
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
 #include "sqr_conv_dev.h"
 
 #ifndef SQR_EXP
@@ -53,6 +54,11 @@ struct D3Args {
   uint32_t xbytes, wbytes;
   unsigned long long* tp;  // nullable: clock probe slots
 };
+
+// one 1-KiB LDS-DMA piece (16 B per lane to dst + 16*lane)
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t srd, char* dst, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(srd, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
 
 // LDS-DMA issue of PIECES 1-KiB pieces per wave: piece i of wave w lands at rows
 // (i*NW + w)*8 .. +7 of dst; per-lane voffsets are fixed, the scalar soffset selects chunk / tap
@@ -1022,6 +1028,45 @@ __device__ __forceinline__ s16x4 ds_read_tr16_off(uint32_t addr) {
   return r;
 }
 
+// compile-time loop: f(std::integral_constant<int, I>{}) for I = B .. E-1
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt field");
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// s_waitcnt vmcnt(m * PER) for m in 0..2 (m wave-uniform; PER pieces per chunk)
+template <int PER>
+__device__ __forceinline__ void wait_vm_chunks(int m) {
+  if (m >= 2) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+  } else if (m == 1) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// wgrad read stream: LDS reads still allowed in flight when step j (of NS per chunk) starts, i.e.
+// the reads issued after step j's X fragments — 2 per step plus 8 dY reads ahead of each sub's
+// tap 0 — by the D-1 steps since; in the last chunk nothing is issued past its end
+constexpr int wg_lgkm(int j, int D, int NS, bool last) {
+  int n = 0;
+  for (int k = j - D + 1; k <= j - 1; ++k) {
+    if (last && k + D >= NS) continue;
+    n += 2 + ((k + D) % 9 == 0 ? 8 : 0);
+  }
+  return n > 15 ? 15 : n;
+}
+
 struct D3WArgs {
   const void* x;   // [N][H][W][C]
   const void* dy;  // [N][H][W][K]
@@ -1030,6 +1075,7 @@ struct D3WArgs {
   int tiles_x, chunks_per_img, nchunks, cps;  // cps = chunks per split
   int ntc, ntiles;                              // C/64, (K/64)*(C/64)
   uint32_t xbytes, dybytes;
+  unsigned long long* tp;  // clock probe (null unless armed)
 };
 
 template <typename T, int TW, int TH, int STAGES>
@@ -1047,6 +1093,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  clock_begin(a.tp);
   const int split = bid / a.ntiles, tile = bid - split * a.ntiles;
   const int k0 = (tile / a.ntc) * 64, c0 = (tile % a.ntc) * 64;
   const int ch0 = split * a.cps;
@@ -1071,6 +1118,9 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     xwx[i] = r % WWID;
     xcol[i] = (c0 + lch * 8) * 2;
   }
+  int xlin[XP];  // window piece offset from the chunk origin's X byte offset (may be negative)
+#pragma unroll
+  for (int i = 0; i < XP; ++i) xlin[i] = xwy[i] < 0 ? 0 : ((xwy[i] - 1) * a.W + xwx[i] - 1) * a.C * 2 + xcol[i];
   const __amdgpu_buffer_rsrc_t xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t dsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, a.dybytes, 0x00020000);
 
@@ -1087,7 +1137,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     _Pragma("unroll") for (int i = 0; i < XP; ++i) {                                                       \
       const int h = h0 - 1 + xwy[i], w = w0 - 1 + xwx[i];                                                  \
       const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;                          \
-      xvo[i] = ok ? (uint32_t)(((img * a.H + h) * a.W + w) * a.C * 2 + xcol[i]) : kOOB;                    \
+      xvo[i] = (uint32_t)(((img * a.H + h) * a.W + w) * a.C * 2 + xcol[i]) | (ok ? 0u : kOOB);             \
     }                                                                                                      \
     dma_pieces<XP, NW>(xsrd, dst_ + TILE_D, xvo, 0, wave);                                                 \
   } while (0)
@@ -1095,20 +1145,27 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   // ---- fragment addressing: lane (fq, fr) reads pixels kk = 32*sub + 8*fq + (fr>>2) (+4) at
   // byte 8*(fr&3) of the 32-B window holding its 16 columns (TN kernel convention)
   const int fr = lane & 15, fq = lane >> 4;
-  int draddr[SUBS][2][4];  // dY fragment offsets in a stage, k-tile kt
-  int xaddr[SUBS][2][3];   // window fragment offsets at tap (0, s); tap (r, s) = +r rows, ^64 if r odd
+  // sub-0 offsets in two row-parity variants: sub s shifts the pixels by (32s/TW rows, 32s%TW
+  // columns) and tap (r, s) the window by r rows more; a column shift of 32 keeps the XOR key and
+  // an odd row shift flips its bit 1 (address bit 6), so every read is sbase + one of these
+  // registers + an immediate offset
+  int dpar[2][2][4];  // [row parity][h][k-tile] dY fragment offsets
+  int xpar[2][2][3];  // [row parity][h][column tap] window fragment offsets
 #pragma unroll
-  for (int sub = 0; sub < SUBS; ++sub)
+  for (int h = 0; h < 2; ++h) {
+    const int kk = 8 * fq + (fr >> 2) + 4 * h;
+    const int py = kk / TW, px = kk % TW;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kk = 32 * sub + 8 * fq + (fr >> 2) + 4 * h;
-      const int py = kk / TW, px = kk % TW;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) draddr[sub][h][kt] = kk * ROWB + ((kt ^ psw(py, px)) << 5) + 8 * (fr & 3);
-#pragma unroll
-      for (int c3 = 0; c3 < 3; ++c3)
-        xaddr[sub][h][c3] = (py * WWID + px + c3) * ROWB + ((wave ^ psw(py, px + c3)) << 5) + 8 * (fr & 3);
+    for (int kt = 0; kt < 4; ++kt) {
+      dpar[0][h][kt] = kk * ROWB + ((kt ^ psw(py, px)) << 5) + 8 * (fr & 3);
+      dpar[1][h][kt] = dpar[0][h][kt] ^ 64;
     }
+#pragma unroll
+    for (int c3 = 0; c3 < 3; ++c3) {
+      xpar[0][h][c3] = (py * WWID + px + c3) * ROWB + ((wave ^ psw(py, px + c3)) << 5) + 8 * (fr & 3);
+      xpar[1][h][c3] = xpar[0][h][c3] ^ 64;
+    }
+  }
 
   f32x4 acc[9][4];
 #pragma unroll
@@ -1116,94 +1173,130 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) acc[t][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-  for (int q = 0; q < STAGES - 1; ++q)
-    if (q < nloc) SQR_W_ISSUE(q, q);
-  if (nloc >= STAGES - 1) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (STAGES - 2)) : "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
+  // The chunk's 9*SUBS steps (sub, tap) run as one flat stream: a step's 4 MFMAs are followed by
+  // the LDS reads of the step D later (its X fragments, and the dY fragments of a new sub), so a
+  // read has D steps (D*64 MFMA cycles) to land before anything waits on it, and the stream
+  // carries across chunk boundaries.  Two barriers per chunk: A at step 0 (every wave is past the
+  // previous chunk's stage -> the DMA for chunk q+STAGES-1 may overwrite it) and T at step NS-D
+  // (chunk q+1 has landed -> its reads may start).  The stage of a chunk is a compile-time
+  // constant (the chunk loop is unrolled by STAGES) so that every read is one of the per-stage
+  // base registers + an immediate: no address arithmetic in the stream (with one wave per SIMD
+  // the instruction issue between the MFMAs is what the stream is short of).
+  constexpr int NS = 9 * SUBS, D = 4;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
-  for (int q = 0; q < nloc; ++q) {
-    const bool more = q + STAGES - 1 < nloc;
-#if SQR_EXP & 2
-    (void)more;
-#else
-    if (more) SQR_W_ISSUE(q + STAGES - 1, (q + STAGES - 1) % STAGES);
-#endif
-    const uint32_t dbase = lds_addr(smem + (q % STAGES) * STAGE), xbase = dbase + TILE_D;
+  s16x4 xlo[9], xhi[9], dlo[2][4], dhi[2][4];
+  uint32_t dps[STAGES][2][2][4], xps[STAGES][2][2][3];
+  {
+    const uint32_t sm0 = lds_addr(smem);
 #pragma unroll
-    for (int sub = 0; sub < SUBS; ++sub) {
-      // software pipeline (one wave per SIMD: nothing else hides LDS latency): the dY fragments
-      // and the X fragments of taps 0-1 are requested up front, then tap t+2's reads are issued
-      // behind tap t's 4 MFMAs and a counted lgkmcnt leaves them in flight
-      s16x4 dlo[4], dhi[4], xlo[9], xhi[9];
+    for (int st = 0; st < STAGES; ++st)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        dlo[kt] = ds_read_tr16(dbase + draddr[sub][0][kt]);
-        dhi[kt] = ds_read_tr16(dbase + draddr[sub][1][kt]);
-      }
-      uint32_t xb[2][3], xb1[2][3];  // tap rows r even / odd
+      for (int par = 0; par < 2; ++par)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int c3 = 0; c3 < 3; ++c3) {
-          xb[h][c3] = xbase + xaddr[sub][h][c3];
-          xb1[h][c3] = xb[h][c3] ^ 64u;
+          for (int kt = 0; kt < 4; ++kt) dps[st][par][h][kt] = sm0 + st * STAGE + dpar[par][h][kt];
+#pragma unroll
+          for (int c3 = 0; c3 < 3; ++c3) xps[st][par][h][c3] = sm0 + st * STAGE + TILE_D + xpar[par][h][c3];
         }
-#define SQR_X_READ(TP)                                                                                 \
-  do {                                                                                                \
-    constexpr int R_ = (TP) / 3, S_ = (TP) % 3, OFF_ = R_ * WWID * ROWB;                                \
-    xlo[TP] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[0][S_] : xb[0][S_]);                                \
-    xhi[TP] = ds_read_tr16_off<OFF_>((R_ & 1) ? xb1[1][S_] : xb[1][S_]);                                \
-  } while (0)
-      SQR_X_READ(0);
-      SQR_X_READ(1);
-      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      V8<T> bfr[4];
+  }
+  auto issue = [&](auto stc, auto jc) __attribute__((always_inline)) {
+    constexpr int ST = decltype(stc)::value, jn = decltype(jc)::value;
+    constexpr int s = jn / 9, t = jn % 9, R = t / 3, S = t % 3;
+    constexpr int DYS = 32 * s / TW, DXS = 32 * s % TW;  // sub s's pixel shift
+    if constexpr (t == 0) {
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        const s16x8 v = {dlo[kt][0], dlo[kt][1], dlo[kt][2], dlo[kt][3], dhi[kt][0], dhi[kt][1], dhi[kt][2], dhi[kt][3]};
-        bfr[kt] = __builtin_bit_cast(V8<T>, v);
+        dlo[s & 1][kt] = ds_read_tr16_off<32 * s * ROWB>(dps[ST][DYS & 1][0][kt]);
+        dhi[s & 1][kt] = ds_read_tr16_off<32 * s * ROWB>(dps[ST][DYS & 1][1][kt]);
       }
-#define SQR_TAP(TP)                                                                                     \
-  do {                                                                                                 \
-    const s16x8 v_ = {xlo[TP][0], xlo[TP][1], xlo[TP][2], xlo[TP][3], xhi[TP][0], xhi[TP][1], xhi[TP][2], xhi[TP][3]}; \
-    const V8<T> afr_ = __builtin_bit_cast(V8<T>, v_);                                                \
-    _Pragma("unroll") for (int kt = 0; kt < 4; ++kt) acc[TP][kt] = mfma(afr_, bfr[kt], acc[TP][kt]);     \
-  } while (0)
-#define SQR_TAP_NEXT(TP)                                  \
-  do {                                                   \
-    SQR_TAP(TP);                                          \
-    SQR_X_READ(TP + 2);                                   \
-    asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");   \
-    __builtin_amdgcn_sched_barrier(0);                   \
-  } while (0)
-      SQR_TAP_NEXT(0);
-      SQR_TAP_NEXT(1);
-      SQR_TAP_NEXT(2);
-      SQR_TAP_NEXT(3);
-      SQR_TAP_NEXT(4);
-      SQR_TAP_NEXT(5);
-      SQR_TAP_NEXT(6);
-      SQR_TAP(7);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    constexpr int XOFF = ((DYS + R) * WWID + DXS) * ROWB;
+    static_assert(XOFF < 65536, "ds offset field");
+    xlo[t] = ds_read_tr16_off<XOFF>(xps[ST][(DYS + R) & 1][0][S]);
+    xhi[t] = ds_read_tr16_off<XOFF>(xps[ST][(DYS + R) & 1][1][S]);
+  };
+  // chunk q in stage ST (= q % STAGES); LAST: no chunk follows
+  int pl_h0 = 0, pl_w0 = 0, pl_dso = 0, pl_xo = 0;  // the DMA in flight: chunk origin, dY / X byte offsets
+  auto chunk = [&](auto stc, auto lastc, int q) __attribute__((always_inline)) {
+    constexpr int ST = decltype(stc)::value, NX = (ST + 1) % STAGES;
+    constexpr bool LAST = decltype(lastc)::value;
+    static_assert(PER < NS - D, "a chunk's DMA pieces are all issued before barrier T");
+    const bool more = q + STAGES - 1 < nloc;
+    static_for<0, NS>([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int s = j / 9, t = j % 9;
+      lgkm_wait<wg_lgkm(j, D, NS, LAST)>();
       __builtin_amdgcn_sched_barrier(0);
-      SQR_TAP(8);
-#undef SQR_TAP_NEXT
-#undef SQR_TAP
-#undef SQR_X_READ
-    }
-    if (more) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER * (STAGES - 2)) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+      const s16x8 xv = {xlo[t][0], xlo[t][1], xlo[t][2], xlo[t][3], xhi[t][0], xhi[t][1], xhi[t][2], xhi[t][3]};
+      const V8<T> afr = __builtin_bit_cast(V8<T>, xv);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const s16x4 &lo = dlo[s & 1][kt], &hi = dhi[s & 1][kt];
+        const s16x8 dv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[t][kt] = mfma(afr, __builtin_bit_cast(V8<T>, dv), acc[t][kt]);
+      }
+      // the DMA of chunk q+STAGES-1 into the stage chunk q-1 used: planned at step 0 (after
+      // barrier A), one 1-KiB piece per step after it so its address math spreads over the MFMAs
+      if constexpr (j == 0) {
+        __builtin_amdgcn_s_barrier();
+        const int ch = ch0 + q + STAGES - 1;
+        const int img = ch / a.chunks_per_img, rem = ch - img * a.chunks_per_img;
+        const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+        pl_h0 = ty * TH;
+        pl_w0 = tx * TW;
+        pl_dso = __builtin_amdgcn_readfirstlane(((img * a.H + pl_h0) * a.W + pl_w0) * a.K * 2);
+        pl_xo = __builtin_amdgcn_readfirstlane(((img * a.H + pl_h0) * a.W + pl_w0) * a.C * 2);
+      }
+#if !(SQR_EXP & 2)
+      if constexpr (j >= 1 && j <= PER) {
+        constexpr int i = j - 1, DST = (ST + STAGES - 1) % STAGES;
+        if (more) {
+          if constexpr (i < DP) {
+            dma_piece(dsrd, smem + DST * STAGE + ((i * NW + wave) * 8) * 128, dvoff[i], pl_dso);
+          } else {
+            constexpr int xi = i - DP;
+            const int h = pl_h0 - 1 + xwy[xi], w = pl_w0 - 1 + xwx[xi];
+            const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+            const uint32_t vo = (uint32_t)(pl_xo + xlin[xi]) | (ok ? 0u : kOOB);
+            dma_piece(xsrd, smem + DST * STAGE + TILE_D + ((xi * NW + wave) * 8) * 128, vo, 0);
+          }
+        }
+      }
+#endif
+      if constexpr (j + D < NS) {
+        issue(stc, std::integral_constant<int, j + D>{});
+      } else if constexpr (!LAST) {
+        if constexpr (j + D == NS) {
+          wait_vm_chunks<PER>(min(STAGES - 2, nloc - q - 2));
+          __builtin_amdgcn_s_barrier();
+        }
+        issue(std::integral_constant<int, NX>{}, std::integral_constant<int, j + D - NS>{});
+      }
+    });
+  };
+
+  if (nloc > 0) {
+#pragma unroll
+    for (int q = 0; q < STAGES - 1; ++q)
+      if (q < nloc) SQR_W_ISSUE(q, q);
+    wait_vm_chunks<PER>(min(STAGES - 2, nloc - 1));
     __builtin_amdgcn_s_barrier();
+    static_for<0, D>([&](auto jc) __attribute__((always_inline)) { issue(std::integral_constant<int, 0>{}, jc); });
+    // groups of STAGES chunks with a successor, then the 1..STAGES remaining ones (the last of them
+    // LAST) — straight-line bodies only: a branch between bodies inside the loop made the compiler
+    // move the accumulators between AGPRs and VGPRs around every chunk
+    int q = 0;
+    for (; q + STAGES < nloc; q += STAGES)
+      static_for<0, STAGES>([&](auto sc) __attribute__((always_inline)) { chunk(sc, std::false_type{}, q + decltype(sc)::value); });
+    const int rem = nloc - q;
+    static_for<1, STAGES + 1>([&](auto rc) __attribute__((always_inline)) {
+      constexpr int RM = decltype(rc)::value;
+      if (rem == RM) {
+        static_for<0, RM - 1>([&](auto sc) __attribute__((always_inline)) { chunk(sc, std::false_type{}, q + decltype(sc)::value); });
+        chunk(std::integral_constant<int, RM - 1>{}, std::true_type{}, q + RM - 1);
+      }
+    });
   }
 
 #undef SQR_W_ISSUE
@@ -1227,6 +1320,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     for (int t = 0; t < 9; ++t) *(f32x4*)(row + t * a.C) = acc[t][kt];
   }
 #endif
+  clock_end(a.tp);
 }
 
 namespace {
@@ -1508,6 +1602,7 @@ int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t 
   a.ntiles = p.ntiles;
   a.xbytes = (uint32_t)((size_t)N * H * W * C * 2);
   a.dybytes = (uint32_t)((size_t)N * H * W * K * 2);
+  a.tp = probe_clock_take();
   *splits = p.splits;
   const dim3 grid(p.splits * p.ntiles), blk(256);
   probe_begin(st);

@@ -11,5 +11,5 @@ mkdir -p build/exp
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -munsafe-fp-atomics -DSQR_EXP=$EXP "$@" \
   -c sq-recovery_amd/csrc/sqr_conv3.hip -o build/exp/sqr_conv3_$EXP.o
 OTHERS=$(ls $OBJ/*.o | grep -v sqr_conv3.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o sq-recovery_amd/sqr/libsqr_exp$EXP.so build/exp/sqr_conv3_$EXP.o $OTHERS
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined -o sq-recovery_amd/sqr/libsqr_exp$EXP.so build/exp/sqr_conv3_$EXP.o $OTHERS
 echo sq-recovery_amd/sqr/libsqr_exp$EXP.so
