@@ -1073,6 +1073,11 @@ extern "C" int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo) {
 static bool direct3(const sqr_conv_desc* d, const Shape& sh) {
   return !sh.im2col && d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1;
 }
+// the direct weight-gradient kernel also takes stride 2 (the first conv of layers 2-4)
+static bool direct3w(const sqr_conv_desc* d, const Shape& sh) {
+  return !sh.im2col && d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && (d->stride == 1 || d->stride == 2) &&
+         d->pad == 1;
+}
 
 extern "C" size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which) {
   Shape sh;
@@ -1083,8 +1088,8 @@ extern "C" size_t sqr_conv2d_workspace_bytes(const sqr_conv_desc* d, int which) 
   const int Ng = sh.im2col ? sh.Kp : d->R * d->S * d->C;
   const TNPlan p = plan_tn(d->K, Ng, sh.M, sh.ES);
   size_t slab = (size_t)p.splits * d->K * Ng * sizeof(float);
-  if (direct3(d, sh)) {
-    const size_t s3 = conv3w_slab_bytes(d->N, d->H, d->W, d->C, d->K);
+  if (direct3w(d, sh)) {
+    const size_t s3 = conv3w_slab_bytes(d->N, d->H, d->W, d->C, d->K, d->stride);
     slab = s3 > slab ? s3 : slab;
   }
   return col + align_up(slab);
@@ -1369,10 +1374,10 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
     a.g = make_gather(x, d->H, d->W, d->C, sh.Ho, sh.Wo, d->stride, -d->pad, -d->pad, 1, d->R, d->S, d->N, sh.ES);
     Ng = d->R * d->S * d->C;
   }
-  if (direct3(d, sh)) {
+  if (direct3w(d, sh)) {
     int splits = 0;
     const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
-    rc = conv3w_launch(d->dtype, x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st);
+    rc = conv3w_launch(d->dtype, x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st, d->stride);
     if (rc == 0) {
       rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st, fin, red,
                                red_lds);

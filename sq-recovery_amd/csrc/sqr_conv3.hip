@@ -1069,20 +1069,40 @@ constexpr int wg_lgkm(int j, int D, int NS, bool last) {
 
 struct D3WArgs {
   const void* x;   // [N][H][W][C]
-  const void* dy;  // [N][H][W][K]
+  const void* dy;  // [N][Ho][Wo][K]
   float* slab;     // [splits][K][9*C]
-  int N, H, W, C, K;
+  int N, H, W, C, K, Ho, Wo;
   int tiles_x, chunks_per_img, nchunks, cps;  // cps = chunks per split
   int ntc, ntiles;                              // C/64, (K/64)*(C/64)
   uint32_t xbytes, dybytes;
   unsigned long long* tp;  // clock probe (null unless armed)
 };
 
-template <typename T, int TW, int TH, int STAGES>
+// X window geometry of the weight-gradient kernel.  Stride 1: one (TH+2) x (TW+2) plane.  Stride
+// 2: the (2TH+1) x (2TW+1) input window as four phase planes (a, b) = (input row, column parity
+// relative to the window origin), plane (a, b) holding TH+1-a rows of width TW+2 (b = 0: TW+1
+// columns + one unused, keeping the width even for the XOR key) or TW (b = 1).  Tap (r, s) of
+// output pixel (py, px) reads plane (r & 1, s & 1) at (py + (r >> 1), px + (s >> 1)): consecutive
+// output pixels are consecutive plane rows, so the stride-1 fragment reads carry over.
+template <int S, int TW, int TH>
+struct WgWin {
+  static constexpr int PH(int a) { return S == 1 ? TH + 2 : TH + 1 - a; }
+  static constexpr int PW(int b) { return S == 1 ? TW + 2 : (b ? TW : TW + 2); }
+  static constexpr int PB(int a, int b) {  // first LDS row of plane (a, b)
+    return S == 1 ? 0 : (a * 2 + b >= 1 ? PH(0) * PW(0) : 0) + (a * 2 + b >= 2 ? PH(0) * PW(1) : 0) +
+                            (a * 2 + b >= 3 ? PH(1) * PW(0) : 0);
+  }
+  static constexpr int ROWS = S == 1 ? PH(0) * PW(0) : PB(1, 1) + PH(1) * PW(1);
+  static constexpr int YO(int r) { return S == 1 ? r : r >> 1; }  // tap -> plane row / column offset
+  static constexpr int PA(int r) { return S == 1 ? 0 : r & 1; }   // tap -> plane parity
+};
+
+template <typename T, int TW, int TH, int STAGES, int S>
 __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   constexpr int NW = 4, ROWB = 128;
   constexpr int BKP = TW * TH, SUBS = BKP / 32;      // pixels per chunk, 32-pixel k-steps
-  constexpr int WWID = TW + 2, WR = (TH + 2) * WWID;
+  using Win = WgWin<S, TW, TH>;
+  constexpr int WR = Win::ROWS;
   constexpr int WROWS = (WR + 31) / 32 * 32;
   constexpr int DP = BKP / 32, XP = WROWS / 32;      // dY / window pieces per wave per chunk
   constexpr int PER = DP + XP;
@@ -1107,40 +1127,34 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   for (int i = 0; i < DP; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // local pixel
     const int lch = 2 * ((pslot >> 1) ^ psw(r / TW, r % TW)) + (pslot & 1);
-    dvoff[i] = (uint32_t)((((r / TW) * a.W + (r % TW)) * a.K + k0 + lch * 8) * 2);
+    dvoff[i] = (uint32_t)((((r / TW) * a.Wo + (r % TW)) * a.K + k0 + lch * 8) * 2);
   }
+  // window LDS row r -> plane (pa, pb), plane position (y, x) -> input offset (iy, ix) from the
+  // chunk's window origin (S*h0 - 1, S*w0 - 1)
   int xwy[XP], xwx[XP], xcol[XP];
 #pragma unroll
   for (int i = 0; i < XP; ++i) {
-    const int r = (i * NW + wave) * 8 + prow;  // window row
-    const int lch = 2 * ((pslot >> 1) ^ psw(r / WWID, r % WWID)) + (pslot & 1);
-    xwy[i] = r < WR ? r / WWID : -(1 << 20);  // padding rows of the LDS window fail the bounds test
-    xwx[i] = r % WWID;
+    const int r = (i * NW + wave) * 8 + prow;
+    int pa = 0, pb = 0;
+    if (S == 2) {
+      pa = r >= Win::PB(1, 0) ? 1 : 0;
+      pb = r >= Win::PB(1, 1) || (r >= Win::PB(0, 1) && r < Win::PB(1, 0)) ? 1 : 0;
+    }
+    const int pbase = pa ? (pb ? Win::PB(1, 1) : Win::PB(1, 0)) : (pb ? Win::PB(0, 1) : Win::PB(0, 0));
+    const int pw = pb ? Win::PW(1) : Win::PW(0);
+    const int y = (r - pbase) / pw, x = (r - pbase) - y * pw;
+    const int lch = 2 * ((pslot >> 1) ^ psw(y, x)) + (pslot & 1);
+    // padding rows of the LDS window and the unused column of the b = 0 planes fail the bounds test
+    const bool used = r < WR && (S == 1 || x < TW + 1 - pb);
+    xwy[i] = used ? S * y + pa : -(1 << 20);
+    xwx[i] = S * x + pb;
     xcol[i] = (c0 + lch * 8) * 2;
   }
   int xlin[XP];  // window piece offset from the chunk origin's X byte offset (may be negative)
 #pragma unroll
-  for (int i = 0; i < XP; ++i) xlin[i] = xwy[i] < 0 ? 0 : ((xwy[i] - 1) * a.W + xwx[i] - 1) * a.C * 2 + xcol[i];
+  for (int i = 0; i < XP; ++i) xlin[i] = xwy[i] < 0 ? 0 : (xwy[i] * a.W + xwx[i]) * a.C * 2 + xcol[i];
   const __amdgpu_buffer_rsrc_t xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t dsrd = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, 0, a.dybytes, 0x00020000);
-
-#define SQR_W_ISSUE(q_, stage_)                                                                              \
-  do {                                                                                                     \
-    const int ch = ch0 + (q_);                                                                             \
-    const int img = ch / a.chunks_per_img, rem = ch - img * a.chunks_per_img;                              \
-    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;                                             \
-    const int h0 = ty * TH, w0 = tx * TW;                                                                  \
-    char* dst_ = smem + (stage_) * STAGE;                                                                  \
-    const int dso = __builtin_amdgcn_readfirstlane(((img * a.H + h0) * a.W + w0) * a.K * 2);               \
-    dma_pieces<DP, NW>(dsrd, dst_, dvoff, dso, wave);                                                      \
-    uint32_t xvo[XP];                                                                                      \
-    _Pragma("unroll") for (int i = 0; i < XP; ++i) {                                                       \
-      const int h = h0 - 1 + xwy[i], w = w0 - 1 + xwx[i];                                                  \
-      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;                          \
-      xvo[i] = (uint32_t)(((img * a.H + h) * a.W + w) * a.C * 2 + xcol[i]) | (ok ? 0u : kOOB);             \
-    }                                                                                                      \
-    dma_pieces<XP, NW>(xsrd, dst_ + TILE_D, xvo, 0, wave);                                                 \
-  } while (0)
 
   // ---- fragment addressing: lane (fq, fr) reads pixels kk = 32*sub + 8*fq + (fr>>2) (+4) at
   // byte 8*(fr&3) of the 32-B window holding its 16 columns (TN kernel convention)
@@ -1150,7 +1164,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   // an odd row shift flips its bit 1 (address bit 6), so every read is sbase + one of these
   // registers + an immediate offset
   int dpar[2][2][4];  // [row parity][h][k-tile] dY fragment offsets
-  int xpar[2][2][3];  // [row parity][h][column tap] window fragment offsets
+  int xpar[2][2][3];  // [row parity][h][column tap] window fragment offsets (row tap 0)
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int kk = 8 * fq + (fr >> 2) + 4 * h;
@@ -1162,7 +1176,9 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     }
 #pragma unroll
     for (int c3 = 0; c3 < 3; ++c3) {
-      xpar[0][h][c3] = (py * WWID + px + c3) * ROWB + ((wave ^ psw(py, px + c3)) << 5) + 8 * (fr & 3);
+      const int pb = Win::PA(c3), xo = Win::YO(c3);
+      xpar[0][h][c3] = (Win::PB(0, pb) + py * Win::PW(pb) + px + xo) * ROWB + ((wave ^ psw(py, px + xo)) << 5) +
+                       8 * (fr & 3);
       xpar[1][h][c3] = xpar[0][h][c3] ^ 64;
     }
   }
@@ -1202,7 +1218,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   }
   auto issue = [&](auto stc, auto jc) __attribute__((always_inline)) {
     constexpr int ST = decltype(stc)::value, jn = decltype(jc)::value;
-    constexpr int s = jn / 9, t = jn % 9, R = t / 3, S = t % 3;
+    constexpr int s = jn / 9, t = jn % 9, R = t / 3, Sc = t % 3;
     constexpr int DYS = 32 * s / TW, DXS = 32 * s % TW;  // sub s's pixel shift
     if constexpr (t == 0) {
 #pragma unroll
@@ -1211,13 +1227,37 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
         dhi[s & 1][kt] = ds_read_tr16_off<32 * s * ROWB>(dps[ST][DYS & 1][1][kt]);
       }
     }
-    constexpr int XOFF = ((DYS + R) * WWID + DXS) * ROWB;
+    constexpr int PB_ = Win::PA(Sc), YR = DYS + Win::YO(R);
+    constexpr int XOFF = (Win::PB(Win::PA(R), PB_) - Win::PB(0, PB_) + YR * Win::PW(PB_) + DXS) * ROWB;
     static_assert(XOFF < 65536, "ds offset field");
-    xlo[t] = ds_read_tr16_off<XOFF>(xps[ST][(DYS + R) & 1][0][S]);
-    xhi[t] = ds_read_tr16_off<XOFF>(xps[ST][(DYS + R) & 1][1][S]);
+    xlo[t] = ds_read_tr16_off<XOFF>(xps[ST][YR & 1][0][Sc]);
+    xhi[t] = ds_read_tr16_off<XOFF>(xps[ST][YR & 1][1][Sc]);
   };
   // chunk q in stage ST (= q % STAGES); LAST: no chunk follows
-  int pl_h0 = 0, pl_w0 = 0, pl_dso = 0, pl_xo = 0;  // the DMA in flight: chunk origin, dY / X byte offsets
+  // the chunk whose DMA is being issued: window origin (input coordinates), dY / X byte offsets
+  int pl_oy = 0, pl_ox = 0, pl_dso = 0, pl_xo = 0;
+  auto plan = [&](int ch) __attribute__((always_inline)) {
+    const int img = ch / a.chunks_per_img, rem = ch - img * a.chunks_per_img;
+    const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
+    const int h0 = ty * TH, w0 = tx * TW;
+    pl_oy = S * h0 - 1;
+    pl_ox = S * w0 - 1;
+    pl_dso = __builtin_amdgcn_readfirstlane(((img * a.Ho + h0) * a.Wo + w0) * a.K * 2);
+    pl_xo = __builtin_amdgcn_readfirstlane(((img * a.H + pl_oy) * a.W + pl_ox) * a.C * 2);
+  };
+  // piece i of the planned chunk into stage st: dY pieces first, then the window's
+  auto piece = [&](auto ic, int st) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    if constexpr (i < DP) {
+      dma_piece(dsrd, smem + st * STAGE + ((i * NW + wave) * 8) * 128, dvoff[i], pl_dso);
+    } else {
+      constexpr int xi = i - DP;
+      const int h = pl_oy + xwy[xi], w = pl_ox + xwx[xi];
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const uint32_t vo = (uint32_t)(pl_xo + xlin[xi]) | (ok ? 0u : kOOB);
+      dma_piece(xsrd, smem + st * STAGE + TILE_D + ((xi * NW + wave) * 8) * 128, vo, 0);
+    }
+  };
   auto chunk = [&](auto stc, auto lastc, int q) __attribute__((always_inline)) {
     constexpr int ST = decltype(stc)::value, NX = (ST + 1) % STAGES;
     constexpr bool LAST = decltype(lastc)::value;
@@ -1240,28 +1280,12 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
       // barrier A), one 1-KiB piece per step after it so its address math spreads over the MFMAs
       if constexpr (j == 0) {
         __builtin_amdgcn_s_barrier();
-        const int ch = ch0 + q + STAGES - 1;
-        const int img = ch / a.chunks_per_img, rem = ch - img * a.chunks_per_img;
-        const int ty = rem / a.tiles_x, tx = rem - ty * a.tiles_x;
-        pl_h0 = ty * TH;
-        pl_w0 = tx * TW;
-        pl_dso = __builtin_amdgcn_readfirstlane(((img * a.H + pl_h0) * a.W + pl_w0) * a.K * 2);
-        pl_xo = __builtin_amdgcn_readfirstlane(((img * a.H + pl_h0) * a.W + pl_w0) * a.C * 2);
+        plan(ch0 + q + STAGES - 1);
       }
 #if !(SQR_EXP & 2)
       if constexpr (j >= 1 && j <= PER) {
         constexpr int i = j - 1, DST = (ST + STAGES - 1) % STAGES;
-        if (more) {
-          if constexpr (i < DP) {
-            dma_piece(dsrd, smem + DST * STAGE + ((i * NW + wave) * 8) * 128, dvoff[i], pl_dso);
-          } else {
-            constexpr int xi = i - DP;
-            const int h = pl_h0 - 1 + xwy[xi], w = pl_w0 - 1 + xwx[xi];
-            const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-            const uint32_t vo = (uint32_t)(pl_xo + xlin[xi]) | (ok ? 0u : kOOB);
-            dma_piece(xsrd, smem + DST * STAGE + TILE_D + ((xi * NW + wave) * 8) * 128, vo, 0);
-          }
-        }
+        if (more) piece(std::integral_constant<int, i>{}, DST);
       }
 #endif
       if constexpr (j + D < NS) {
@@ -1279,7 +1303,10 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   if (nloc > 0) {
 #pragma unroll
     for (int q = 0; q < STAGES - 1; ++q)
-      if (q < nloc) SQR_W_ISSUE(q, q);
+      if (q < nloc) {
+        plan(ch0 + q);
+        static_for<0, PER>([&](auto ic) __attribute__((always_inline)) { piece(ic, q); });
+      }
     wait_vm_chunks<PER>(min(STAGES - 2, nloc - 1));
     __builtin_amdgcn_s_barrier();
     static_for<0, D>([&](auto jc) __attribute__((always_inline)) { issue(std::integral_constant<int, 0>{}, jc); });
@@ -1299,7 +1326,6 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     });
   }
 
-#undef SQR_W_ISSUE
 
   // ---- epilogue: lane holds dW[k = k0+16kt+fr][tap t][c = c0+16w+4fq .. +3]
   const size_t ng = (size_t)9 * a.C;
@@ -1552,18 +1578,31 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
 // ---------------------------------------------------------------- weight-gradient launcher
 namespace {
 struct D3WPlan {
-  int TW, TH, splits, cps, nchunks, chunks_per_img, tiles_x, ntiles;
+  int TW, TH, splits, cps, nchunks, chunks_per_img, tiles_x, ntiles, Ho, Wo;
 };
-bool plan_w(int N, int H, int W, int C, int K, D3WPlan* p) {
-  if (g_direct == 0 || C % 64 || K % 64 || W < 8 || pow2_log(W) < 0) return false;
-  // chunks of 128 pixels (64 for W = 8): a taller window amortises its halo rows
-  const int TW = W >= 64 ? 64 : W, TH = TW == 8 ? 8 : 128 / TW;
-  if (H % TH) return false;
-  if ((size_t)N * H * W * (C > K ? C : K) * 2 >= (1u << 31)) return false;
+bool plan_w(int N, int H, int W, int C, int K, int stride, D3WPlan* p) {
+  if (g_direct == 0 || C % 64 || K % 64 || (stride != 1 && stride != 2)) return false;
+  if (stride == 2 && (H % 2 || W % 2)) return false;
+  const int Ho = H / stride, Wo = W / stride;
+  if (Wo < 8 || pow2_log(Wo) < 0) return false;
+  // stride 1: chunks of 128 pixels (64 for W = 8), a taller window amortising its halo rows;
+  // stride 2: 64-pixel chunks (the four-plane window of a 128-pixel chunk would not fit 3 stages)
+  int TW, TH;
+  if (stride == 1) {
+    TW = Wo >= 64 ? 64 : Wo;
+    TH = TW == 8 ? 8 : 128 / TW;
+  } else {
+    TW = Wo >= 32 ? 32 : Wo;
+    TH = 64 / TW;
+  }
+  if (Ho % TH) return false;
+  if ((size_t)N * H * W * C * 2 >= (1u << 31) || (size_t)N * Ho * Wo * K * 2 >= (1u << 31)) return false;
   p->TW = TW;
   p->TH = TH;
-  p->tiles_x = W / TW;
-  p->chunks_per_img = (H / TH) * p->tiles_x;
+  p->Ho = Ho;
+  p->Wo = Wo;
+  p->tiles_x = Wo / TW;
+  p->chunks_per_img = (Ho / TH) * p->tiles_x;
   p->nchunks = N * p->chunks_per_img;
   p->ntiles = (K / 64) * (C / 64);
   int splits = (256 + p->ntiles - 1) / p->ntiles;  // one workgroup per CU
@@ -1574,16 +1613,16 @@ bool plan_w(int N, int H, int W, int C, int K, D3WPlan* p) {
 }
 }  // namespace
 
-size_t conv3w_slab_bytes(int N, int H, int W, int C, int K) {
+size_t conv3w_slab_bytes(int N, int H, int W, int C, int K, int stride) {
   D3WPlan p;
-  if (!plan_w(N, H, W, C, K, &p)) return 0;
+  if (!plan_w(N, H, W, C, K, stride, &p)) return 0;
   return (size_t)p.splits * K * 9 * C * sizeof(float);
 }
 
 int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t slab_bytes, int N, int H, int W, int C,
-                  int K, int* splits, hipStream_t st) {
+                  int K, int* splits, hipStream_t st, int stride) {
   D3WPlan p;
-  if (!plan_w(N, H, W, C, K, &p)) return kNotHandled;
+  if (!plan_w(N, H, W, C, K, stride, &p)) return kNotHandled;
   if ((size_t)p.splits * K * 9 * C * sizeof(float) > slab_bytes) return kNotHandled;
   D3WArgs a;
   a.x = x;
@@ -1594,6 +1633,8 @@ int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t 
   a.W = W;
   a.C = C;
   a.K = K;
+  a.Ho = p.Ho;
+  a.Wo = p.Wo;
   a.tiles_x = p.tiles_x;
   a.chunks_per_img = p.chunks_per_img;
   a.nchunks = p.nchunks;
@@ -1601,17 +1642,25 @@ int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t 
   a.ntc = C / 64;
   a.ntiles = p.ntiles;
   a.xbytes = (uint32_t)((size_t)N * H * W * C * 2);
-  a.dybytes = (uint32_t)((size_t)N * H * W * K * 2);
+  a.dybytes = (uint32_t)((size_t)N * p.Ho * p.Wo * K * 2);
   a.tp = probe_clock_take();
   *splits = p.splits;
   const dim3 grid(p.splits * p.ntiles), blk(256);
   probe_begin(st);
   SQR_DISPATCH16(dtype, T, {
-    switch (p.TW) {
-      case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 64, 2, 3>), grid, blk, 0, st, a); break;
-      case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 32, 4, 3>), grid, blk, 0, st, a); break;
-      case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 16, 8, 3>), grid, blk, 0, st, a); break;
-      default: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 8, 8, 4>), grid, blk, 0, st, a); break;
+    if (stride == 1) {
+      switch (p.TW) {
+        case 64: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 64, 2, 3, 1>), grid, blk, 0, st, a); break;
+        case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 32, 4, 3, 1>), grid, blk, 0, st, a); break;
+        case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 16, 8, 3, 1>), grid, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 8, 8, 4, 1>), grid, blk, 0, st, a); break;
+      }
+    } else {
+      switch (p.TW) {
+        case 32: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 32, 2, 3, 2>), grid, blk, 0, st, a); break;
+        case 16: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 16, 4, 3, 2>), grid, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3_wgrad_kernel<T, 8, 8, 3, 2>), grid, blk, 0, st, a); break;
+      }
     }
   });
   probe_end(st);

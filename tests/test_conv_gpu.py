@@ -299,6 +299,27 @@ def test_conv3s2_dgrad_bench_size_vs_f64(shape, dtype):
     assert _rel(dx, dxr) <= (8e-3 if dtype == torch.bfloat16 else 1e-3)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape", [(64, 64, 64, 128), (64, 128, 32, 256), (64, 256, 16, 512), (2, 64, 64, 128),
+                                   (3, 128, 32, 256), (1, 256, 16, 512), (2, 64, 128, 64)],
+                         ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv3s2_wgrad_vs_f64(shape, dtype):
+    """The direct stride-2 weight gradient (four phase planes of the input window; layers 2-4's
+    first conv) at the bench batch and at a few images (few chunks per split, several tiles per
+    row at 128 input) vs float64."""
+    from sqr import conv as sc
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(11 * N + C + K + H)
+    x = torch.randn(N, C, H, H, generator=g).to(dtype).float()
+    gy = torch.randn(N, K, H // 2, H // 2, generator=g).to(dtype).float()
+    d = sc._desc(N, C, H, H, K, 3, 3, 2, 1, dtype)
+    dw = sc.conv2d_bwd_weight(x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last),
+                              gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last), d)
+    torch.cuda.synchronize()
+    dwr = torch.nn.grad.conv2d_weight(x.double(), (K, C, 3, 3), gy.double(), stride=2, padding=1)
+    assert _rel(dw, dwr) <= 2e-4
+
+
 @pytest.mark.parametrize("shape", [(64, 128, 32, 128), (64, 256, 16, 256), (64, 512, 8, 512)],
                          ids=lambda s: "N%dC%dH%dK%d" % s)
 def test_conv3_tiled_bench_size_vs_f64(shape):
