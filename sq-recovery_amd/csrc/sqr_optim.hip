@@ -36,6 +36,7 @@ struct Job {
   int n;            // elements
   int K, C, RS, Kp; // conv geometry (krsc != null)
   int f16;          // krsc element type: 0 bf16, 1 fp16
+  int vec;          // p, m, v, g 16-B aligned (and conv rows a multiple of 4): float4 path
 };
 struct Jobs {
   Job j[MAXJ];
@@ -72,31 +73,81 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   const double t = (double)(*jb.step) + 1.0;
   const double bc1 = 1.0 - pow(J.b1, t), bc2 = 1.0 - pow(J.b2, t);
   const float step_size = (float)(J.lr / bc1), bc2s = (float)sqrt(bc2);
+  // Adam is HBM-bound (28 B per element): the float4 path keeps 16 loads of 16 B in flight per
+  // thread (2 groups x p, m, v, g), the scalar path (unaligned slots, odd sizes) 4 of 4 B
+  auto upd4 = [&](size_t i4, float* keep) {  // elements 4*i4 .. +3
+    f32x4 p = ((const f32x4*)jb.p)[i4], m = ((const f32x4*)jb.m)[i4], v = ((const f32x4*)jb.v)[i4];
+    const f32x4 g = ((const f32x4*)jb.g)[i4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = p[e], me = m[e], ve = v[e];
+      adam_update(pe, me, ve, gsc == 1.f ? g[e] : g[e] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+      p[e] = pe;
+      m[e] = me;
+      v[e] = ve;
+      if (keep) keep[e] = pe;
+    }
+    ((f32x4*)jb.p)[i4] = p;
+    ((f32x4*)jb.m)[i4] = m;
+    ((f32x4*)jb.v)[i4] = v;
+  };
+  auto upd1 = [&](size_t i) {
+    float p = jb.p[i], m = jb.m[i], v = jb.v[i];
+    adam_update(p, m, v, gsc == 1.f ? jb.g[i] : jb.g[i] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
+    jb.p[i] = p;
+    jb.m[i] = m;
+    jb.v[i] = v;
+    return p;
+  };
   if (!jb.krsc) {
     const int i0 = local * CHUNK;
     const int i1 = min(i0 + CHUNK, jb.n);
-    for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) {
-      float p = jb.p[i], m = jb.m[i], v = jb.v[i];
-      adam_update(p, m, v, gsc == 1.f ? jb.g[i] : jb.g[i] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
-      jb.p[i] = p;
-      jb.m[i] = m;
-      jb.v[i] = v;
+    if (jb.vec) {  // CHUNK = 256 threads x 2 float4; the job's tail (n % 4) in scalar
+      const int q1 = i1 >> 2;
+#pragma unroll
+      for (int u = 0; u < CHUNK / 1024; ++u) {
+        const int q = (i0 >> 2) + u * 256 + (int)threadIdx.x;
+        if (q < q1) upd4(q, nullptr);
+      }
+      if (i1 == jb.n && (int)threadIdx.x < (jb.n & 3)) upd1((size_t)(jb.n & ~3) + threadIdx.x);
+    } else {
+      for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) upd1(i);
     }
     return;
   }
   // conv weight: row k = local, CRS = C * RS contiguous elements w[k][c][tap]
   const int k = local, CRS = jb.C * jb.RS;
   const size_t base = (size_t)k * CRS;
-  for (int i = threadIdx.x; i < CRS; i += 256) {
-    float p = jb.p[base + i], m = jb.m[base + i], v = jb.v[base + i];
-    adam_update(p, m, v, gsc == 1.f ? jb.g[base + i] : jb.g[base + i] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s, J.eps);
-    jb.p[base + i] = p;
-    jb.m[base + i] = m;
-    jb.v[base + i] = v;
-    lds[i] = p;
+  if (jb.vec) {
+    const int n4 = CRS >> 2;
+    for (int q = threadIdx.x; q < n4; q += 512) {
+      upd4((base >> 2) + q, lds + 4 * q);
+      if (q + 256 < n4) upd4((base >> 2) + q + 256, lds + 4 * (q + 256));
+    }
+  } else {
+    for (int i = threadIdx.x; i < CRS; i += 256) lds[i] = upd1(base + i);
   }
   __syncthreads();
   // krsc[k][tap][c] (row length Kp >= RS*C; the im2col padding is zero)
+  if (jb.vec && jb.Kp == CRS && (jb.C & 7) == 0) {  // 8 channels of one tap per 16-B store
+    for (int i = 8 * threadIdx.x; i < CRS; i += 2048) {
+      const int tap = i / jb.C, c = i - tap * jb.C;
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = lds[(c + 2 * e) * jb.RS + tap], hi = lds[(c + 2 * e + 1) * jb.RS + tap];
+        if (jb.f16) {
+          typedef f16 h2 __attribute__((ext_vector_type(2)));
+          w[e] = __builtin_bit_cast(uint32_t, h2{(f16)lo, (f16)hi});
+        } else {
+          typedef bf16 b2 __attribute__((ext_vector_type(2)));
+          w[e] = __builtin_bit_cast(uint32_t, b2{(bf16)lo, (bf16)hi});
+        }
+      }
+      *(u32x4*)((uint16_t*)jb.krsc + (size_t)k * jb.Kp + i) = u32x4{w[0], w[1], w[2], w[3]};
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < jb.Kp; i += 256) {
     float val = 0.f;
     if (i < CRS) {
@@ -212,6 +263,11 @@ extern "C" int sqr_adam_step_amp(const sqr_adam_param* params, int nparams, doub
       jb.krsc = q.w_krsc;
       jb.f16 = q.desc.dtype == SQR_DTYPE_F16;
       jb.K = jb.C = jb.RS = jb.Kp = 0;
+      {
+        const uintptr_t orp = (uintptr_t)q.p | (uintptr_t)q.g | (uintptr_t)q.exp_avg | (uintptr_t)q.exp_avg_sq;
+        jb.vec = (orp & 15) == 0;
+        if (q.w_krsc) jb.vec = jb.vec && ((q.desc.C * q.desc.R * q.desc.S) & 3) == 0;
+      }
       int nb;
       if (q.w_krsc) {
         const sqr_conv_desc& d = q.desc;

@@ -99,7 +99,7 @@ class GraphDataParallel:
         off = 0
         for p in order:
             members.append(id(p))
-            off += p.numel()
+            off = gradbuf.slot_end(id(p))
             if off - start >= cap:
                 self.buckets.append((start, off, members))
                 start, members = off, []

@@ -13,16 +13,28 @@ _slots = {}  # id(param) -> (flat buffer, element offset, shape)
 _listener = [None]  # called with the ids of parameters whose gradients were just enqueued
 
 
+ALIGN = 64  # elements: every slot starts 256-B aligned (the fused Adam's float4 path needs 16 B)
+
+
+def slot_end(param_id):
+    """Element offset just past the parameter's slot padding (the next slot's start)."""
+    flat, off, shape = _slots[param_id]
+    n = 1
+    for v in shape:
+        n *= v
+    return off + (n + ALIGN - 1) // ALIGN * ALIGN
+
+
 def install(params, device):
-    """Allocate the flat buffer for `params` (in the given order) and register their slots.
-    Returns the buffer."""
+    """Allocate the flat buffer for `params` (in the given order) and register their slots; each
+    slot starts at a multiple of ALIGN elements (the padding stays zero).  Returns the buffer."""
     params = list(params)
-    n = sum(p.numel() for p in params)
+    n = sum((p.numel() + ALIGN - 1) // ALIGN * ALIGN for p in params)
     flat = torch.zeros(n, dtype=torch.float32, device=device)
     off = 0
     for p in params:
         _slots[id(p)] = (flat, off, tuple(p.shape))
-        off += p.numel()
+        off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
     return flat
 
 
