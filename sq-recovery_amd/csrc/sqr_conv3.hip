@@ -26,10 +26,8 @@
 #ifndef SQR_EXP
 #define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop;
                    // conv3_kernel: 4 no per-tap wait/barrier, 8 no MFMA, 16 no fragment reads;
-                   // conv3p_kernel: 128 no tap loop, 256 no output stores, 512 no row loads in
-                   // the tile loop, 1024 no fragment reads, 16384 no weight prologue, 32768 no
-                   // BatchNorm partials, 65536 per-wave phase cycle sums into the clock probe
-                   // buffer (tools/conv_phase.py); conv3s2_dgrad_kernel: 2048 no dX
+                   // conv3p_kernel: 128 no MFMAs, 256 no output stores, 512 no row loads in
+                   // the tile loop; conv3s2_dgrad_kernel: 2048 no dX
                    // stores, 4096 no MFMA, 8192 no weight loads after the prologue)
 #endif
 
@@ -473,17 +471,6 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   char* const ring = smem;
   char* const stg = ring + RING;
   clock_begin(a.tp);
-#if SQR_EXP & 65536  // per-wave phase cycle sums (s_memtime) -> a.tp[2 + (block*4 + wave)*10 + phase]
-  unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, pt = __builtin_amdgcn_s_memtime();
-#define SQR_PH(i)                                                \
-  {                                                              \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    ph[i] += t_ - pt;                                            \
-    pt = t_;                                                     \
-  }
-#else
-#define SQR_PH(i)
-#endif
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -527,6 +514,12 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       }
     }
   };
+  auto load_row_piece = [&](int r0, int i, u32x4* v, bool use) {  // piece i of 2 rows (RPW per wave)
+    const int p = i * NW + wave;
+    uint32_t vo;
+    row_piece(r0, p, &vo, use && p < 2 * PPR);
+    v[i] = __builtin_amdgcn_raw_buffer_load_b128(xsrd, vo, 0, 0);
+  };
   auto write_rows = [&](int r0, int nrows, const u32x4* v) {
 #pragma unroll
     for (int i = 0; i < (4 * PPR + NW - 1) / NW; ++i) {
@@ -555,24 +548,19 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       bmu[e] = a.bn_mean[(tid & 7) * 8 + e];
     }
   }
-  auto load_addend = [&](int k) {
+  auto load_addend_piece = [&](int k, int q) {
     const size_t tile0 = ((size_t)img * H + hb + k * TH) * TW * BN;  // first element of tile k
     const char* src = (const char*)(BNB ? a.bn_x : a.addend) + tile0 * 2;
-#pragma unroll
-    for (int q = 0; q < NST; ++q) av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
-    if constexpr (BNB) {
-#pragma unroll
-      for (int q = 0; q < NST; ++q) bm[q] = a.bn_mask[tile0 / 8 + q * NT + tid];
-    }
+    av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
+    if constexpr (BNB) bm[q] = a.bn_mask[tile0 / 8 + q * NT + tid];
   };
   // (use = false: a tile that does not exist -- the stores go out of the buffer's range and are
   // dropped; issuing them anyway keeps the vector-memory instruction count the same on every path,
   // so the compiler's vmcnt waits for the row registers never include these stores)
   const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.xbytes, 0x00020000);
-  auto store_staged = [&](int k, bool use) {
+  auto store_piece = [&](int k, bool use, int q) {
     const uint32_t dst = use ? (uint32_t)(((img * H + hb + k * TH) * TW * BN) * 2) : kOOB;
-#pragma unroll
-    for (int q = 0; q < NST; ++q) {
+    {
       const int c = q * NT + tid, row = c >> 3, slot = c & 7;
       u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
       if constexpr (ACC) {
@@ -598,6 +586,10 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         __builtin_amdgcn_raw_buffer_store_b128(v, osrd, dst | (uint32_t)(c * 16), 0, 0);
     }
   };
+  auto store_staged = [&](int k, bool use) {
+#pragma unroll
+    for (int q = 0; q < NST; ++q) store_piece(k, use, q);
+  };
 
   // Weights resident in REGISTERS: a wave's MFMA A operands for all 36 (tap, 16-channel slice)
   // steps (its 32 output channels x 576 = 36 KiB, 144 VGPRs; one wave per SIMD has 512), read once
@@ -606,7 +598,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // lane half h.
   const int r32 = lane & 31, h = lane >> 5;
   V8<T> wreg[36];
-  u32x4 rv[RPW];  // the next tile's new rows, loaded one tile ahead
+  // rvb[t & 1]: the new rows of tile t, loaded during tile t-2's MFMA loop, written to the ring at the
+  // end of tile t-1 (about 1.5 tiles of load latency hidden)
+  u32x4 rvb[2][RPW];
   {
     u32x4 t0[(4 * PPR + NW - 1) / NW], wv[WPW];
     load_rows(hb - 1, 4, t0, true);  // tile 0: rows hb-1 .. hb+2
@@ -624,7 +618,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // tile 1's new rows (written during tile 0).  Row loads are always the last vector-memory
   // instructions before the loop head, so the compiler's vmcnt waits for them are exact on both
   // paths into the loop (a younger store would make it wait for the store as well)
-  load_rows(hb + 3, 2, rv, ntile > 1);
+  load_rows(hb + 3, 2, rvb[1], ntile > 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   {
@@ -633,21 +627,14 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int s = 0; s < 36; ++s)
       wreg[s] = *(const V8<T>*)(wl + (s >> 2) * BN * ROWB + prow32 + (((2 * (s & 3) + h) ^ pkey) << 4));
   }
-  SQR_PH(0);
 
-  for (int k = 0; k < ntile; ++k) {
-    // tile k+1's new rows (loaded during tile k-1) go into the slots tile k-2's rows used (free
-    // since the last barrier; visible to every wave after this tile's barriers); then tile k+2's
-    // rows are loaded into the same registers
-    if (k + 1 < ntile) write_rows(hb + 2 * (k + 1) + 1, 2, rv);
-    SQR_PH(9);
-    store_staged(k - 1, k >= 1);
-    if constexpr (ACC || BNB) load_addend(k);
-    SQR_PH(1);
-#if !(SQR_EXP & 512)
-    load_rows(hb + 2 * (k + 2) + 1, 2, rv, k + 2 < ntile);
-#endif
-    SQR_PH(8);
+  // One tile = 36 MFMA steps.  Its vector-memory work is spread over those steps instead of issued
+  // in bursts at the tile boundary (every workgroup runs in lock-step with the others, so bursts
+  // leave HBM idle during the MFMA loops and saturated in between: the kernel without its MFMA loop
+  // takes 11-13 us, with it 23-27 us): the 4 staged stores of tile k-1 at steps 1 + 8q, the row
+  // loads of tile k+2 at steps 3 + 7i, the addend / BatchNorm-input loads of tile k at 5 + 8q.
+  auto tile = [&](int k, auto par) {
+    constexpr int P = decltype(par)::value;  // k & 1 (static: selects the row buffers)
     f32x16 acc[TM];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -662,29 +649,28 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       const int rr = flip ? 2 - r : r, cc = flip ? 2 - c3 : c3;
       const int slot = 2 * kk + h;
       const int lrow0 = ((rbase + rr) & (NSLOT - 1)) * SLOTR + cc + r32;
-#if SQR_EXP & 1024
-#pragma unroll
-      for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)(lrow0 + i), 0u, 0u, 0u});
-#else
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int L = lrow0 + 32 * i;
         qf[i] = *(const V8<T>*)(ring + L * ROWB + ((slot ^ ((L >> 1) & 7)) << 4));
       }
-#endif
     };
     constexpr int NSTEP = 36, PD = 2;
     V8<T> qf[PD + 1][TM];
 #pragma unroll
     for (int s = 0; s < PD; ++s) load(s, qf[s]);
-#if SQR_EXP & 128
-    if (ntile < 0)
-#endif
 #pragma unroll
     for (int s = 0; s < NSTEP; ++s) {
+      if (s % 8 == 1) store_piece(k - 1, k >= 1 && !(SQR_EXP & 256), s / 8);
+      if (s % 7 == 3 && s / 7 < RPW)
+        load_row_piece(hb + 2 * (k + 2) + 1, s / 7, rvb[P], k + 2 < ntile && !(SQR_EXP & 512));
+      if constexpr (ACC || BNB)
+        if (s % 8 == 5) load_addend_piece(k, s / 8);
       if (s + PD < NSTEP) load(s + PD, qf[(s + PD) % (PD + 1)]);
+#if !(SQR_EXP & 128)
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[i] = mfma32(wreg[s], qf[s % (PD + 1)][i], acc[i]);
+#endif
 #pragma unroll
       for (int g = 0; g < TM; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // a fragment read
@@ -693,7 +679,6 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    SQR_PH(2);
     // lane holds D[n = wn*32 + 8g + 4h + e][pixel wm*64 + 32i + r32], g = reg >> 2, e = reg & 3
     uint32_t pk[TM][4][2];
 #pragma unroll
@@ -702,7 +687,6 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       for (int g = 0; g < 4; ++g) {
         pk[i][g][0] = pack2<T>(acc[i][4 * g], acc[i][4 * g + 1]);
         pk[i][g][1] = pack2<T>(acc[i][4 * g + 2], acc[i][4 * g + 3]);
-#if !(SQR_EXP & 32768)
 #pragma unroll
         for (int q = 0; q < 2 * STATS; ++q) {
           const float v0 = lo2f<T>(pk[i][g][q]), v1 = hi2f<T>(pk[i][g][q]);
@@ -711,13 +695,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
           st1[4 * g + 2 * q + 1] += v1;
           st2[4 * g + 2 * q + 1] = fmaf(v1, v1, st2[4 * g + 2 * q + 1]);
         }
-#endif
       }
-    SQR_PH(3);
-    SQR_PH(4);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // tile k+1's rows written (read after barrier 2)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // all waves are done with tile k's rows and the staging area
-    SQR_PH(5);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = wm * WM + 32 * i + r32;
@@ -728,9 +708,14 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         *(u32x2*)(stg + m * ROWB + ((((n >> 3) ^ key) << 4) | ((n & 7) << 1))) = u32x2{pk[i][g][0], pk[i][g][1]};
       }
     }
+    // tile k+1's new rows (loaded during tile k-1) into the slots of tile k-3's rows
+    if (k + 1 < ntile) write_rows(hb + 2 * (k + 1) + 1, 2, rvb[1 - P]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // staged tile and tile k+1's rows visible
-    SQR_PH(6);
+  };
+  for (int k = 0; k < ntile; k += 2) {
+    tile(k, std::integral_constant<int, 0>{});
+    if (k + 1 < ntile) tile(k + 1, std::integral_constant<int, 1>{});
   }
   if (ntile > 0) store_staged(ntile - 1, true);
   // the per-workgroup statistics reductions below reuse the ring: every wave is past its last ring
@@ -758,7 +743,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = col_sum(red + sl * 16 + 8 * q + e, NT / 8, 8 * 16);
     }
   }
-  if (STATS && !(SQR_EXP & 32768)) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
+  if (STATS) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
     float* red = (float*)ring;
     float* r1 = red + (wm * 32 + r32) * BN + wn * WN + 4 * h;
     float* r2 = r1 + 64 * BN;
@@ -775,14 +760,6 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if SQR_EXP & 65536
-  SQR_PH(7);
-  if (a.tp && lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) a.tp[2 + (blockIdx.x * NW + wave) * 10 + i] = ph[i];
-  }
-#endif
-#undef SQR_PH
   clock_end(a.tp);
 }
 
