@@ -99,6 +99,7 @@ class Trainer:
         elif world > 1:
             self.model = dist.wrap(self.net, dev)
             self.use_graph = False
+        self.grad_seed = torch.ones((), dtype=torch.float64, device=dev)
         self.dp_note = None
         self.graph = None
         self.static_loss = None
@@ -115,7 +116,8 @@ class Trainer:
 
     def body(self):
         loss, _ = self.forward_loss()
-        (self.scaler.scale(loss) if self.scaler is not None else loss).backward()
+        # d loss / d loss = 1 from a persistent tensor (autograd would fill a fresh one every step)
+        (self.scaler.scale(loss) if self.scaler is not None else loss).backward(self.grad_seed)
         if self.gdp is not None:
             self.gdp.allreduce()
         if self.scaler is not None:

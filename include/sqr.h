@@ -86,6 +86,18 @@ int sqr_implicit_loss_fwd_bwd(const float* params, const float* target, int B, i
                               float tau, float sharpness, int need_grad, double* loss_per_sample,
                               float* grad_params, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The same plus loss_mean [1] f64 = mean_b loss_per_sample (the reference's returned value,
+ * classes.py:293-295) from the finalize launch itself (B <= 1024; otherwise one more launch).
+ * loss_mean may be NULL. */
+int sqr_implicit_loss_fwd_bwd_mean(const float* params, const float* target, int B, int H, int W, int R,
+                                   float tau, float sharpness, int need_grad, double* loss_per_sample,
+                                   double* loss_mean, float* grad_params, void* workspace,
+                                   size_t workspace_bytes, void* stream);
+
+/* Autograd backward of the losses: out[i] = grad[i] * (float)(*gout) for the f64 upstream gradient
+ * gout of the scalar loss (one launch; out may alias grad). */
+int sqr_loss_grad_scale(const float* grad, const double* gout, long long n, float* out, void* stream);
+
 /* depth_projection only: images [B,R,R] f32 in the reference's image orientation (row = R-1-y, col = x). */
 int sqr_implicit_render(const float* params, int B, int R, float tau, float sharpness, float* images,
                         void* stream);
@@ -97,6 +109,10 @@ size_t sqr_explicit_loss_workspace_bytes(int B, int R);
 int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pred, int B, int R, int need_grad,
                               double* loss_per_sample, float* grad_pred, void* workspace,
                               size_t workspace_bytes, void* stream);
+/* ... with the batch mean (as sqr_implicit_loss_fwd_bwd_mean) */
+int sqr_explicit_loss_fwd_bwd_mean(const float* p_true, const float* p_pred, int B, int R, int need_grad,
+                                   double* loss_per_sample, double* loss_mean, float* grad_pred, void* workspace,
+                                   size_t workspace_bytes, void* stream);
 
 /* IoUAccuracy(R): per-sample voxel counts [B,2] int64 = (|in_true & in_pred|, |in_true | in_pred|),
  * computed in float64 like the reference. */

@@ -661,11 +661,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int s = 0; s < PD; ++s) load(s, qf[s]);
 #pragma unroll
     for (int s = 0; s < NSTEP; ++s) {
-      if (s % 8 == 1) store_piece(k - 1, k >= 1 && !(SQR_EXP & 256), s / 8);
+      if (s % 8 == 1 && s / 8 < NST) store_piece(k - 1, k >= 1 && !(SQR_EXP & 256), s / 8);
       if (s % 7 == 3 && s / 7 < RPW)
         load_row_piece(hb + 2 * (k + 2) + 1, s / 7, rvb[P], k + 2 < ntile && !(SQR_EXP & 512));
       if constexpr (ACC || BNB)
-        if (s % 8 == 5) load_addend_piece(k, s / 8);
+        if (s % 8 == 5 && s / 8 < NST) load_addend_piece(k, s / 8);
       if (s + PD < NSTEP) load(s + PD, qf[(s + PD) % (PD + 1)]);
 #if !(SQR_EXP & 128)
 #pragma unroll

@@ -316,19 +316,68 @@ __device__ void finalize_sample(const float* __restrict__ p, const double* acc, 
   for (int i = 0; i < 12; ++i) grad[i] = (float)(g[i] * gscale * mask[i]);
 }
 
+// batch mean of the per-sample losses in a fixed order (64-lane xor tree, then the waves in order)
+__device__ __forceinline__ void block_mean(double v, int B, double* __restrict__ loss_mean) {
+  __shared__ double wsum[16];
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += wsum[w];
+    *loss_mean = t / (double)B;
+  }
+}
+
+// loss_mean (nullable): the reference's batch mean (classes.py:293-295), computed here when the whole
+// batch is one block (B <= 1024) instead of a separate reduction launch
 __global__ void loss_finalize_kernel(const float* __restrict__ params, const float* __restrict__ partials,
                                      int B, int nblk, double loss_scale, double grad_scale, int need_grad,
-                                     double* __restrict__ loss_out, float* __restrict__ grad_out) {
+                                     double* __restrict__ loss_out, float* __restrict__ grad_out,
+                                     double* __restrict__ loss_mean) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  double acc[kNAcc];
-  for (int i = 0; i < kNAcc; ++i) acc[i] = 0.0;
-  for (int k = 0; k < nblk; ++k) {
-    const float* src = partials + ((size_t)b * nblk + k) * kNAcc;
-    for (int i = 0; i < kNAcc; ++i) acc[i] += (double)src[i];
+  double loss = 0.0;
+  if (b < B) {
+    double acc[kNAcc];
+    for (int i = 0; i < kNAcc; ++i) acc[i] = 0.0;
+    for (int k = 0; k < nblk; ++k) {
+      const float* src = partials + ((size_t)b * nblk + k) * kNAcc;
+      for (int i = 0; i < kNAcc; ++i) acc[i] += (double)src[i];
+    }
+    loss = acc[17] * loss_scale;
+    loss_out[b] = loss;
+    if (need_grad) finalize_sample(params + 12 * b, acc, grad_scale, grad_out + 12 * b);
   }
-  loss_out[b] = acc[17] * loss_scale;
-  if (need_grad) finalize_sample(params + 12 * b, acc, grad_scale, grad_out + 12 * b);
+  if (loss_mean && gridDim.x == 1) block_mean(loss, B, loss_mean);
+}
+
+// batch mean for B > 1024 (one block, fixed order)
+__global__ void __launch_bounds__(1024) loss_mean_kernel(const double* __restrict__ loss_out, int B,
+                                                         double* __restrict__ loss_mean) {
+  double v = 0.0;
+  for (int b = threadIdx.x; b < B; b += 1024) v += loss_out[b];
+  block_mean(v, B, loss_mean);
+}
+
+// d loss / d params scaled by the upstream gradient of the (float64) loss: out = g * (float)*gout
+__global__ void grad_scale_kernel(const float* __restrict__ g, const double* __restrict__ gout, long long n,
+                                  float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = g[i] * (float)*gout;
+}
+
+// one launch of the finalize (+ the batch mean when loss_mean != NULL)
+static void launch_finalize(hipStream_t st, const float* params, const float* partials, int B, int nblk,
+                            double loss_scale, double grad_scale, int need_grad, double* loss_out, float* grad_out,
+                            double* loss_mean) {
+  if (loss_mean && B <= 1024) {
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3((B + 63) / 64 * 64), 0, st, params, partials, B, nblk,
+                       loss_scale, grad_scale, need_grad, loss_out, grad_out, loss_mean);
+    return;
+  }
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3((B + 63) / 64), dim3(64), 0, st, params, partials, B, nblk,
+                     loss_scale, grad_scale, need_grad, loss_out, grad_out, (double*)nullptr);
+  if (loss_mean) hipLaunchKernelGGL(loss_mean_kernel, dim3(1), dim3(1024), 0, st, loss_out, B, loss_mean);
 }
 
 // forward render only: images[b][r][c]
@@ -495,10 +544,10 @@ extern "C" size_t sqr_implicit_loss_workspace_bytes(int B, int R) {
   return (size_t)B * nblk * kNAcc * sizeof(float);
 }
 
-extern "C" int sqr_implicit_loss_fwd_bwd(const float* params, const float* target, int B, int H, int W,
-                                         int R, float tau, float sharpness, int need_grad,
-                                         double* loss_per_sample, float* grad_params, void* workspace,
-                                         size_t workspace_bytes, void* stream) {
+extern "C" int sqr_implicit_loss_fwd_bwd_mean(const float* params, const float* target, int B, int H, int W,
+                                              int R, float tau, float sharpness, int need_grad,
+                                              double* loss_per_sample, double* loss_mean, float* grad_params,
+                                              void* workspace, size_t workspace_bytes, void* stream) {
   SQR_CHECK_ARG(B >= 1 && B <= 65535, "implicit_loss: B=%d out of range [1,65535]", B);
   SQR_CHECK_ARG(R >= 2, "implicit_loss: R=%d must be >= 2", R);
   SQR_CHECK_ARG(!need_grad || R <= 256, "implicit_loss: R=%d > 256 not supported with grad", R);
@@ -533,9 +582,26 @@ extern "C" int sqr_implicit_loss_fwd_bwd(const float* params, const float* targe
   }
   SQR_HIP_LAUNCH_CHECK("implicit_loss_kernel");
   const double rr = (double)R * (double)R;
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3((B + 63) / 64), dim3(64), 0, st, params, partials, B, nblk,
-                     1.0 / rr, 1.0 / ((double)B * rr), need_grad, loss_per_sample, grad_params);
+  launch_finalize(st, params, partials, B, nblk, 1.0 / rr, 1.0 / ((double)B * rr), need_grad, loss_per_sample,
+                  grad_params, loss_mean);
   SQR_HIP_LAUNCH_CHECK("loss_finalize_kernel");
+  return SQR_OK;
+}
+
+extern "C" int sqr_implicit_loss_fwd_bwd(const float* params, const float* target, int B, int H, int W,
+                                         int R, float tau, float sharpness, int need_grad,
+                                         double* loss_per_sample, float* grad_params, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
+  return sqr_implicit_loss_fwd_bwd_mean(params, target, B, H, W, R, tau, sharpness, need_grad, loss_per_sample,
+                                        nullptr, grad_params, workspace, workspace_bytes, stream);
+}
+
+extern "C" int sqr_loss_grad_scale(const float* grad, const double* gout, long long n, float* out, void* stream) {
+  SQR_CHECK_ARG(grad && gout && out && n >= 0, "loss_grad_scale: null pointer or negative size");
+  if (n == 0) return SQR_OK;
+  hipLaunchKernelGGL(grad_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), grad,
+                     gout, n, out);
+  SQR_HIP_LAUNCH_CHECK("grad_scale_kernel");
   return SQR_OK;
 }
 
@@ -564,9 +630,10 @@ extern "C" size_t sqr_explicit_loss_workspace_bytes(int B, int R) {
   return (size_t)B * nblk * kNAcc * sizeof(float);
 }
 
-extern "C" int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pred, int B, int R,
-                                         int need_grad, double* loss_per_sample, float* grad_pred,
-                                         void* workspace, size_t workspace_bytes, void* stream) {
+extern "C" int sqr_explicit_loss_fwd_bwd_mean(const float* p_true, const float* p_pred, int B, int R,
+                                              int need_grad, double* loss_per_sample, double* loss_mean,
+                                              float* grad_pred, void* workspace, size_t workspace_bytes,
+                                              void* stream) {
   SQR_CHECK_ARG(B >= 1 && B <= 65535 && R >= 1 && R <= 1024, "explicit_loss: bad B=%d R=%d", B, R);
   SQR_CHECK_ARG(p_true && p_pred && loss_per_sample && workspace, "explicit_loss: null pointer");
   SQR_CHECK_ARG(!need_grad || grad_pred, "explicit_loss: null grad_pred");
@@ -588,10 +655,17 @@ extern "C" int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pre
                        n, step, partials);
   SQR_HIP_LAUNCH_CHECK("explicit_loss_kernel");
   const double n3 = (double)n * n * n;
-  hipLaunchKernelGGL(loss_finalize_kernel, dim3((B + 63) / 64), dim3(64), 0, st, p_pred, partials, B, nblk,
-                     100.0 / n3, 100.0 / (n3 * (double)B), need_grad, loss_per_sample, grad_pred);
+  launch_finalize(st, p_pred, partials, B, nblk, 100.0 / n3, 100.0 / (n3 * (double)B), need_grad, loss_per_sample,
+                  grad_pred, loss_mean);
   SQR_HIP_LAUNCH_CHECK("loss_finalize_kernel");
   return SQR_OK;
+}
+
+extern "C" int sqr_explicit_loss_fwd_bwd(const float* p_true, const float* p_pred, int B, int R,
+                                         int need_grad, double* loss_per_sample, float* grad_pred,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+  return sqr_explicit_loss_fwd_bwd_mean(p_true, p_pred, B, R, need_grad, loss_per_sample, nullptr, grad_pred,
+                                        workspace, workspace_bytes, stream);
 }
 
 template <typename P>

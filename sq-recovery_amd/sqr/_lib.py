@@ -74,10 +74,15 @@ SIGNATURES = {
     "sqr_implicit_loss_workspace_bytes": (c_size_t, [c_int, c_int]),
     "sqr_implicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float,
                                           c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_implicit_loss_fwd_bwd_mean": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_float, c_float,
+                                               c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_loss_grad_scale": (c_int, [c_void_p, c_void_p, ctypes.c_longlong, c_void_p, c_void_p]),
     "sqr_implicit_render": (c_int, [c_void_p, c_int, c_int, c_float, c_float, c_void_p, c_void_p]),
     "sqr_explicit_loss_workspace_bytes": (c_size_t, [c_int, c_int]),
     "sqr_explicit_loss_fwd_bwd": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                           c_void_p, c_size_t, c_void_p]),
+    "sqr_explicit_loss_fwd_bwd_mean": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                               c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_iou_counts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sqr_iou_counts_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "sqr_conv2d_out_hw": (c_int, [ctypes.POINTER(SqrConvDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),

@@ -1,7 +1,8 @@
 """Autograd wrappers of the fused HIP losses (libsqr: sqr_implicit_loss_fwd_bwd & co).
 
 The kernels compute the loss AND its parameter gradient in one pass (the gradient is
-d(batch-mean loss)/d params); backward() only scales it by the upstream gradient.
+d(batch-mean loss)/d params); the batch mean itself comes out of the same finalize launch, and
+backward() only scales the gradient by the upstream gradient (one sqr_loss_grad_scale launch).
 Reference: torch/classes.py:109-295 (timoblak/sq-recovery).
 """
 import torch
@@ -13,6 +14,17 @@ def _require_cuda(*ts):
     for t in ts:
         if not t.is_cuda:
             raise ValueError("sqr GPU loss called with a CPU tensor (device %s)" % t.device)
+
+
+def _scale_grad(grad, gout, dtype):
+    """grad * gout (gout: the scalar loss's upstream gradient, any float dtype) in one launch."""
+    g = gout.to(torch.float64) if gout.dtype != torch.float64 else gout
+    if not g.is_cuda or g.numel() != 1:
+        return (grad * gout.to(torch.float32)).to(dtype)
+    out = torch.empty_like(grad)
+    check(lib().sqr_loss_grad_scale(ptr(grad), ptr(g), grad.numel(), ptr(out), stream_ptr(grad.device)),
+          "sqr_loss_grad_scale")
+    return out if dtype == torch.float32 else out.to(dtype)
 
 
 class ImplicitLossFn(torch.autograd.Function):
@@ -39,25 +51,25 @@ class ImplicitLossFn(torch.autograd.Function):
         t = tgt.detach().to(torch.float32).contiguous()
         need_grad = bool(ctx.needs_input_grad[1])
         loss_ps = torch.empty(B, dtype=torch.float64, device=p.device)
+        loss = torch.empty((), dtype=torch.float64, device=p.device)  # the batch mean
         grad = torch.empty(B, 12, dtype=torch.float32, device=p.device) if need_grad else None
         L = lib()
         wsb = L.sqr_implicit_loss_workspace_bytes(B, R)
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=p.device)
-        check(L.sqr_implicit_loss_fwd_bwd(ptr(p), ptr(t), B, H, W, int(R), float(tau), float(sharpness),
-                                          int(need_grad), ptr(loss_ps), ptr(grad), ptr(ws), wsb,
-                                          stream_ptr(p.device)), "sqr_implicit_loss_fwd_bwd")
+        check(L.sqr_implicit_loss_fwd_bwd_mean(ptr(p), ptr(t), B, H, W, int(R), float(tau), float(sharpness),
+                                               int(need_grad), ptr(loss_ps), ptr(loss), ptr(grad), ptr(ws), wsb,
+                                               stream_ptr(p.device)), "sqr_implicit_loss_fwd_bwd_mean")
         ctx.save_for_backward(grad)
         ctx.params_dtype = params.dtype
         ctx.per_sample = loss_ps
-        return loss_ps.mean()
+        return loss
 
     @staticmethod
     def backward(ctx, gout):
         (grad,) = ctx.saved_tensors
         if grad is None:
             return None, None, None, None, None
-        g = (grad * gout.to(torch.float32)).to(ctx.params_dtype)
-        return None, g, None, None, None
+        return None, _scale_grad(grad, gout, ctx.params_dtype), None, None, None
 
 
 class ExplicitLossFn(torch.autograd.Function):
@@ -74,22 +86,24 @@ class ExplicitLossFn(torch.autograd.Function):
         pp = p_pred.detach().to(torch.float32).contiguous()
         need_grad = bool(ctx.needs_input_grad[1])
         loss_ps = torch.empty(B, dtype=torch.float64, device=pp.device)
+        loss = torch.empty((), dtype=torch.float64, device=pp.device)  # the batch mean
         grad = torch.empty(B, 12, dtype=torch.float32, device=pp.device) if need_grad else None
         L = lib()
         wsb = L.sqr_explicit_loss_workspace_bytes(B, R)
         ws = torch.empty(max(wsb, 16), dtype=torch.uint8, device=pp.device)
-        check(L.sqr_explicit_loss_fwd_bwd(ptr(pt), ptr(pp), B, int(R), int(need_grad), ptr(loss_ps), ptr(grad),
-                                          ptr(ws), wsb, stream_ptr(pp.device)), "sqr_explicit_loss_fwd_bwd")
+        check(L.sqr_explicit_loss_fwd_bwd_mean(ptr(pt), ptr(pp), B, int(R), int(need_grad), ptr(loss_ps), ptr(loss),
+                                               ptr(grad), ptr(ws), wsb, stream_ptr(pp.device)),
+              "sqr_explicit_loss_fwd_bwd_mean")
         ctx.save_for_backward(grad)
         ctx.params_dtype = p_pred.dtype
-        return loss_ps.mean()
+        return loss
 
     @staticmethod
     def backward(ctx, gout):
         (grad,) = ctx.saved_tensors
         if grad is None:
             return None, None, None
-        return None, (grad * gout.to(torch.float32)).to(ctx.params_dtype), None
+        return None, _scale_grad(grad, gout, ctx.params_dtype), None
 
 
 def implicit_loss(target, params, R, tau=1.0, sharpness=100.0):
