@@ -143,6 +143,9 @@ __device__ __forceinline__ void rows_dot(const float* __restrict__ W, const floa
   }
 }
 
+#ifndef SQR_TAIL_RB
+#define SQR_TAIL_RB 16  // weight rows per batch of loads in flight (per wave) in the fc layers
+#endif
 template <typename T>
 __global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict__ save, float* __restrict__ out_a,
                                                        float* __restrict__ out_e, float* __restrict__ out_t,
@@ -176,9 +179,9 @@ __global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict_
     sv[c] = s;
   }
   __syncthreads();
-  rows_dot<16>(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
+  rows_dot<SQR_TAIL_RB>(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
   __syncthreads();
-  rows_dot<16>(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
+  rows_dot<SQR_TAIL_RB>(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
   __syncthreads();
   for (int i = wave; i < NOUT; i += 4) {
     const int hd = head_of(i), r = head_row(i);
