@@ -379,7 +379,13 @@ __device__ __forceinline__ void pool_load(PoolIn& pi, const T* __restrict__ dpoo
 }
 
 template <typename TI, typename T>
-__global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__ img, const float* __restrict__ w,
+#ifndef SQR_STEM_BWD_OCC
+#define SQR_STEM_BWD_OCC 2  // workgroups per CU the backward's registers are sized for
+#endif
+#ifndef SQR_STEM_BWD_GRID
+#define SQR_STEM_BWD_GRID GRID_PERSIST  // persistent backward grid (<= GRID_PERSIST: workspace rows)
+#endif
+__global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const TI* __restrict__ img, const float* __restrict__ w,
                                                           const T* __restrict__ dpool,
                                                           const T* __restrict__ ypool,
                                                           const uint8_t* __restrict__ argmax, int H, int W, int Hp,
@@ -734,7 +740,7 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N
   hipStream_t st = as_stream(stream);
   float* part = (float*)workspace;
   const int tiles_x = g.Wc / 32, tiles_img = (g.Hc / 4) * tiles_x, ntiles = N * tiles_img;
-  const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;
+  const int grid = ntiles < SQR_STEM_BWD_GRID ? ntiles : SQR_STEM_BWD_GRID;
   SQR_STEM_DISPATCH(x_dtype, y_dtype,
                     hipLaunchKernelGGL((stem_bwd_kernel<TI, T>), dim3(grid), dim3(256), 0, st, (const TI*)x, w,
                                        (const T*)dy, (const T*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles,
