@@ -2,6 +2,8 @@
 of world size 1 (the all-reduce runs, as an identity) — gradients land in the flat buffer, the
 eager step equals plain training bitwise, and the whole step including the RCCL all-reduce is
 captured and replayed as one HIP graph with the same parameter trajectory."""
+import gc
+
 import numpy as np
 import pytest
 import torch
@@ -39,7 +41,7 @@ def test_graph_dp_world1(tmp_path):
     from sqr import gradbuf, losses
     tdist.init_process_group("nccl", init_method="file://%s" % (tmp_path / "store"), rank=0, world_size=1,
                              device_id=torch.device(DEV))
-    g = None
+    g = gdp = static = None
     try:
         rng = np.random.default_rng(0)
         p = torch.tensor(classes.sample_sq_params(rng, 8), device=DEV)
@@ -73,7 +75,18 @@ def test_graph_dp_world1(tmp_path):
         for pa, pb in zip(a_net.parameters(), b_net.parameters()):
             assert (pa - pb).abs().max().item() <= 1e-5 * max(pa.abs().max().item(), 1e-3)
     finally:
-        gradbuf.clear()
+        # teardown order: drain the device, free the captured graph (it holds RCCL work) and every
+        # object that references its memory pool, then the communicator (a destroy with live
+        # captured collectives can abort inside RCCL)
         torch.cuda.synchronize()
-        del g  # the graph holds captured RCCL work: release it before the communicator
+        if gdp is not None:
+            gdp.close(b_opt)
+        gradbuf.clear()
+        if g is not None:
+            g.reset()
+        del g, static, gdp
+        gc.collect()
+        torch.cuda.synchronize()
+        tdist.barrier()
+        torch.cuda.synchronize()
         tdist.destroy_process_group()
