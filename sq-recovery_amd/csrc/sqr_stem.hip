@@ -563,17 +563,18 @@ __global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const T
 }
 
 // ---------------------------------------------------------------- S4: closed-form BN backward
-// (a) column sums of the per-block partials in float64, rows in a fixed order: block = 64 columns
-// (16 float4) x 16 row lanes, the 16 lane sums added in order through LDS
+// (a) column sums of the per-block partials in float64, rows in a fixed order: block = 32 columns
+// (8 float4) x 32 row lanes (262 blocks for the 8,384 columns: every CU streams), the 32 lane sums
+// added in order through LDS
 __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int rows, int cols,
                                                      double* __restrict__ out) {
-  __shared__ double red[16][64];
-  const int q = threadIdx.x & 15, z = threadIdx.x >> 4;
-  const int c0 = blockIdx.x * 64 + 4 * q;
+  __shared__ double red[32][32];
+  const int q = threadIdx.x & 7, z = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * 32 + 4 * q;
   double a[4] = {0.0, 0.0, 0.0, 0.0};
   if (c0 < cols) {
 #pragma unroll 8
-    for (int r = z; r < rows; r += 16) {
+    for (int r = z; r < rows; r += 32) {
       const f32x4 v = *(const f32x4*)(part + (size_t)r * cols + c0);
 #pragma unroll
       for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
@@ -582,10 +583,10 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
 #pragma unroll
   for (int e = 0; e < 4; ++e) red[z][4 * q + e] = a[e];
   __syncthreads();
-  if (threadIdx.x < 64 && blockIdx.x * 64 + (int)threadIdx.x < cols) {
+  if (threadIdx.x < 32 && blockIdx.x * 32 + (int)threadIdx.x < cols) {
     double s = 0.0;
-    for (int zz = 0; zz < 16; ++zz) s += red[zz][threadIdx.x];
-    out[blockIdx.x * 64 + threadIdx.x] = s;
+    for (int zz = 0; zz < 32; ++zz) s += red[zz][threadIdx.x];
+    out[blockIdx.x * 32 + threadIdx.x] = s;
   }
 }
 
@@ -747,7 +748,7 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N
                                        part));
   SQR_HIP_LAUNCH_CHECK("stem_bwd_kernel");
   double* tot = (double*)((char*)workspace + a256((size_t)GRID_PERSIST * PART_BWD * 4));
-  hipLaunchKernelGGL(colsum_kernel, dim3((PART_BWD + 63) / 64), dim3(256), 0, st, (const float*)part, grid, PART_BWD,
+  hipLaunchKernelGGL(colsum_kernel, dim3((PART_BWD + 31) / 32), dim3(256), 0, st, (const float*)part, grid, PART_BWD,
                      tot);
   SQR_HIP_LAUNCH_CHECK("colsum_kernel");
   hipLaunchKernelGGL(stem_bwd_finalize_kernel, dim3(KC), dim3(64), 0, st, (const double*)tot,
