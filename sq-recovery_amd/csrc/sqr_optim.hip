@@ -195,12 +195,18 @@ __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
   const int tap = local / jb.ntk;
   const int r = tap / jb.S, s = tap - r * jb.S;
   const int k0 = tk * 64, c0 = tc * 64;
-  // load krsc[k0 + kk][tap][c0 .. c0 + 63]: thread = (kk = tid / 4, 16 channels)
+  // load krsc[k0 + kk][tap][c0 .. c0 + 63]: thread = (kk = tid / 4, 16 channels = two 16-B loads)
   {
     const int kk = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
-    const uint16_t* src = jb.krsc + ((size_t)(k0 + kk) * RS + tap) * jb.C + c0 + cc;
+    const u32x4* src = (const u32x4*)(jb.krsc + ((size_t)(k0 + kk) * RS + tap) * jb.C + c0 + cc);
+    const u32x4 v0 = src[0], v1 = src[1];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) tile[kk][cc + e] = src[e];
+    for (int e = 0; e < 4; ++e) {
+      tile[kk][cc + 2 * e] = (uint16_t)v0[e];
+      tile[kk][cc + 2 * e + 1] = (uint16_t)(v0[e] >> 16);
+      tile[kk][cc + 8 + 2 * e] = (uint16_t)v1[e];
+      tile[kk][cc + 8 + 2 * e + 1] = (uint16_t)(v1[e] >> 16);
+    }
   }
   __syncthreads();
   // parity class of this tap and its (t, u) inside the class
@@ -213,8 +219,14 @@ __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
   {
     const int cc = threadIdx.x >> 2, kk = (threadIdx.x & 3) * 16;
     uint16_t* dst = jb.crsk + jb.cls_off[cl] + (((size_t)(c0 + cc) * Rc + t) * Sc + u) * jb.K + k0 + kk;
+    u32x4 w0, w1;  // 16 consecutive k of channel c0 + cc: two 16-B stores (K, k0, kk multiples of 16)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) dst[e] = tile[kk + e][cc];
+    for (int e = 0; e < 4; ++e) {
+      w0[e] = (uint32_t)tile[kk + 2 * e][cc] | ((uint32_t)tile[kk + 2 * e + 1][cc] << 16);
+      w1[e] = (uint32_t)tile[kk + 8 + 2 * e][cc] | ((uint32_t)tile[kk + 8 + 2 * e + 1][cc] << 16);
+    }
+    ((u32x4*)dst)[0] = w0;
+    ((u32x4*)dst)[1] = w1;
   }
 }
 
