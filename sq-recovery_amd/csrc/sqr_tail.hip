@@ -18,6 +18,7 @@
 // transposed products (W^T d) split the reduction over the 4 waves and add the 4 parts in order.
 // Every sum has a fixed order: results are bitwise reproducible.
 #include <stdint.h>
+#include <stdlib.h>
 #include "sqr_common.h"
 
 namespace sqr {
@@ -146,15 +147,11 @@ __device__ __forceinline__ void rows_dot(const float* __restrict__ W, const floa
 #ifndef SQR_TAIL_RB
 #define SQR_TAIL_RB 16  // weight rows per batch of loads in flight (per wave) in the fc layers
 #endif
+// average pool of sample n into feat[C0] (LDS; thread = (pixel phase, 8-channel vector), phases *
+// C0 == 2048), also written to sv when sv != null
 template <typename T>
-__global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict__ save, float* __restrict__ out_a,
-                                                       float* __restrict__ out_e, float* __restrict__ out_t,
-                                                       float* __restrict__ out_q) {
-  __shared__ float feat[MAXF], h0[MAXF], h1[MAXF], red[2048], z[16];
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float* sv = save + (size_t)n * d.ldsave;
-
-  // average pool: thread = (pixel phase, 8-channel vector); phases * C0 == 2048
+__device__ __forceinline__ void pool_sample(const Dev& d, int n, float* feat, float* red, float* sv) {
+  const int tid = threadIdx.x;
   const int V = d.C0 >> 3, phases = 256 / V;
   const int v = tid % V, ph = tid / V;
   {
@@ -176,13 +173,15 @@ __global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict_
     for (int q = 0; q < phases; ++q) s += red[q * d.C0 + c];
     s = s / (float)d.P;
     feat[c] = s;
-    sv[c] = s;
+    if (sv) sv[c] = s;
   }
   __syncthreads();
-  rows_dot<SQR_TAIL_RB>(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
-  __syncthreads();
-  rows_dot<SQR_TAIL_RB>(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
-  __syncthreads();
+}
+
+// the four heads of sample n from h1 (LDS): logits into sv, activated outputs
+__device__ __forceinline__ void heads_sample(const Dev& d, int n, const float* h1, float* z, float* sv, float* out_a,
+                                             float* out_e, float* out_t, float* out_q) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = wave; i < NOUT; i += 4) {
     const int hd = head_of(i), r = head_row(i);
     const float s = wave_dot(d.wh[hd] + (size_t)r * d.F2, h1, d.F2, lane) + d.bh[hd][r];
@@ -202,6 +201,61 @@ __global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict_
       out_q[n * 4 + tid - 8] = zi / nrm;
     }
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) tail_fwd_kernel(Dev d, float* __restrict__ save, float* __restrict__ out_a,
+                                                       float* __restrict__ out_e, float* __restrict__ out_t,
+                                                       float* __restrict__ out_q) {
+  __shared__ float feat[MAXF], h0[MAXF], h1[MAXF], red[2048], z[16];
+  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* sv = save + (size_t)n * d.ldsave;
+  pool_sample<T>(d, n, feat, red, sv);
+  rows_dot<SQR_TAIL_RB>(d.w0, d.b0, feat, d.F1, d.C0, wave, lane, sv + d.C0, h0);
+  __syncthreads();
+  rows_dot<SQR_TAIL_RB>(d.w1, d.b1, h0, d.F2, d.F1, wave, lane, sv + d.C0 + d.F1, h1);
+  __syncthreads();
+  heads_sample(d, n, h1, z, sv, out_a, out_e, out_t, out_q);
+  (void)tid;
+}
+
+// The same forward as three launches with 4 workgroups per sample in the two linear layers: the
+// single-kernel form is a chain of dependent L2 round trips per sample (4 row batches per wave in
+// each layer) on 64 workgroups; here each workgroup owns a quarter of a layer's rows (one batch per
+// wave) and the layers meet through the save buffer (pre-activations; leaky recomputed on load).
+//   fc0: grid (B, 4): pool the sample, rows [q*F1/4, (q+1)*F1/4) of encoder.fc.0
+//   fc1: grid (B, 4): h0 = leaky(save fc0), rows [q*F2/4, ..) of encoder.fc.2
+//   heads: grid B:    h1 = leaky(save fc1), the four heads
+template <typename T>
+__global__ void __launch_bounds__(256) tail_fc0_kernel(Dev d, float* __restrict__ save) {
+  __shared__ float feat[MAXF], act[MAXF], red[2048];
+  const int n = blockIdx.x, q = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* sv = save + (size_t)n * d.ldsave;
+  pool_sample<T>(d, n, feat, red, q == 0 ? sv : nullptr);
+  const int rows = d.F1 >> 2, r0 = q * rows;
+  rows_dot<SQR_TAIL_RB>(d.w0 + (size_t)r0 * d.C0, d.b0 + r0, feat, rows, d.C0, wave, lane, sv + d.C0 + r0, act);
+}
+
+__global__ void __launch_bounds__(256) tail_fc1_kernel(Dev d, float* __restrict__ save) {
+  __shared__ float h0[MAXF], act[MAXF];
+  const int n = blockIdx.x, q = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* sv = save + (size_t)n * d.ldsave;
+  for (int k = threadIdx.x; k < d.F1; k += 256) h0[k] = leaky(sv[d.C0 + k]);
+  __syncthreads();
+  const int rows = d.F2 >> 2, r0 = q * rows;
+  rows_dot<SQR_TAIL_RB>(d.w1 + (size_t)r0 * d.F1, d.b1 + r0, h0, rows, d.F1, wave, lane, sv + d.C0 + d.F1 + r0,
+                        act);
+}
+
+__global__ void __launch_bounds__(256) tail_heads_kernel(Dev d, float* __restrict__ save, float* __restrict__ out_a,
+                                                         float* __restrict__ out_e, float* __restrict__ out_t,
+                                                         float* __restrict__ out_q) {
+  __shared__ float h1[MAXF], z[16];
+  const int n = blockIdx.x;
+  float* sv = save + (size_t)n * d.ldsave;
+  for (int k = threadIdx.x; k < d.F2; k += 256) h1[k] = leaky(sv[d.C0 + d.F1 + k]);
+  __syncthreads();
+  heads_sample(d, n, h1, z, sv, out_a, out_e, out_t, out_q);
 }
 
 struct Up {  // upstream gradients of a, e, t, q (nullable = zero) and their row strides
@@ -452,6 +506,22 @@ extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a,
   SQR_CHECK_ARG(x && out_a && out_e && out_t && out_q && save, "tail_fwd: null pointer");
   const Dev d = make_dev(t, x);
   hipStream_t st = as_stream(stream);
+  static const int split = [] {
+    const char* e = getenv("SQR_TAIL_SPLIT");
+    return e ? atoi(e) : 1;
+  }();
+  if (split && t->F1 % 16 == 0 && t->F2 % 16 == 0) {  // three launches, 4 workgroups per sample in fc0 / fc1
+    if (t->dtype == SQR_DTYPE_BF16)
+      hipLaunchKernelGGL(tail_fc0_kernel<bf16>, dim3(t->B, 4), dim3(256), 0, st, d, save);
+    else if (t->dtype == SQR_DTYPE_F16)
+      hipLaunchKernelGGL(tail_fc0_kernel<f16>, dim3(t->B, 4), dim3(256), 0, st, d, save);
+    else
+      hipLaunchKernelGGL(tail_fc0_kernel<float>, dim3(t->B, 4), dim3(256), 0, st, d, save);
+    hipLaunchKernelGGL(tail_fc1_kernel, dim3(t->B, 4), dim3(256), 0, st, d, save);
+    hipLaunchKernelGGL(tail_heads_kernel, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
+    SQR_HIP_LAUNCH_CHECK("tail_fc0/fc1/heads_kernel");
+    return 0;
+  }
   if (t->dtype == SQR_DTYPE_BF16)
     hipLaunchKernelGGL(tail_fwd_kernel<bf16>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
   else if (t->dtype == SQR_DTYPE_F16)

@@ -48,7 +48,12 @@ class BasicBlock(nn.Module):
         # the identity / downsample branch's gradient of x is added in conv1's backward-data
         # epilogue through a ResidualJoin instead of a separate add)
         join = ResidualJoin.make(x) if _JOIN else None
-        link = BnBackwardLink.make(x, self.bn1) if _BN_LINK else None
+        # bn1's backward reduction in conv2's backward-data epilogue pays off up to 64x64 maps (the
+        # persistent layer-1 kernel at 256x256 input and every deeper layer); the tiled kernel on the
+        # 128x128 layer-1 maps of 512x512 input runs 118 -> 212 us with it (same-box A/B of config 5:
+        # +0.9 % without the link), so larger maps keep bn1's own reduction pass
+        hw = (x.shape[2] // self.stride) * (x.shape[3] // self.stride)
+        link = BnBackwardLink.make(x, self.bn1) if (_BN_LINK and hw <= 64 * 64) else None
         # x's producer (the previous block's output BatchNorm) may have its backward reduction ride
         # on conv1's weight-gradient launch (BnOutLink)
         red_link = getattr(x, "_sqr_outlink", None) if join is not None else None
