@@ -23,6 +23,7 @@ from .conv import BnBackwardLink, BnOutLink, Conv2d, ResidualJoin, compute_dtype
 _JOIN = os.environ.get("SQR_RESIDUAL_JOIN", "1") != "0"
 _BN_ADD = os.environ.get("SQR_BN_ADD", "1") != "0"
 _BN_LINK = os.environ.get("SQR_BN_LINK", "1") != "0"
+_JOIN_MAXHW = int(os.environ.get("SQR_JOIN_MAXHW", str(1 << 30)))  # experiments: largest map with the join
 
 
 class BasicBlock(nn.Module):
@@ -47,7 +48,7 @@ class BasicBlock(nn.Module):
         # (training: each conv's epilogue also emits the batch statistics its BN needs; backward:
         # the identity / downsample branch's gradient of x is added in conv1's backward-data
         # epilogue through a ResidualJoin instead of a separate add)
-        join = ResidualJoin.make(x) if _JOIN else None
+        join = ResidualJoin.make(x) if (_JOIN and x.shape[2] * x.shape[3] <= _JOIN_MAXHW) else None
         # bn1's backward reduction in conv2's backward-data epilogue pays off up to 64x64 maps (the
         # persistent layer-1 kernel at 256x256 input and every deeper layer); the tiled kernel on the
         # 128x128 layer-1 maps of 512x512 input runs 118 -> 212 us with it (same-box A/B of config 5:
