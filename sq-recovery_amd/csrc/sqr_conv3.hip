@@ -418,13 +418,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 // ============================================================================ layer-1 persistent
 // Cin = Nout = 64, W = 64 (ResNetSQ layer1, forward and backward-data).  One workgroup per band of
 // consecutive 2-row tiles of one image (B = 64: a quarter image = 8 tiles per workgroup):
-//  * the whole 3x3 weight tensor (9 x 64 x 64 bf16 = 72 KiB) is resident in LDS;
+//  * each wave's share of the 3x3 weights (its 32 output channels x 576, 36 MFMA fragments) is
+//    loaded once (through a coalesced LDS image in the prologue) and held in VGPRs;
 //  * input rows live in an 8-slot LDS ring (slot = (row + 1) & 7; one image row + its 2 zero halo
-//    columns per slot): a tile reads 4 rows of which only 2 are new, and the new rows of the next
-//    TWO tiles stream in by LDS-DMA while the current tile computes, so every input row is fetched
-//    once per band and two tiles of loads are always in flight;
-//  * the output tile is staged in LDS and written with 16-B coalesced stores that drain while the
-//    next tile computes; BatchNorm partials accumulate in registers, one partial row per workgroup.
+//    columns per slot): a tile reads 4 rows of which only 2 are new; the new rows of tile k+2 are
+//    loaded into registers during tile k's MFMA loop and written to the ring at the end of tile
+//    k+1, so every input row is fetched once per band;
+//  * the output tile is staged in LDS and written with 16-B coalesced stores during the next
+//    tile's MFMA loop; BatchNorm partials accumulate in registers, one partial row per workgroup.
 struct D3PArgs {
   const void* x;   // [N][H][64][64]
   const void* w;   // [64][9][64]
