@@ -177,7 +177,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   };
   u32x2 av[ACC || BNB ? TN : 1][ACC || BNB ? TM : 1];
   uint32_t bmk[BNB ? TN : 1][BNB ? TM : 1];
-  if constexpr (ACC || BNB) {
+  // LATE: 4-wave workgroups with 64 x 64 wave tiles (TM * TN >= 16) load the addend / BatchNorm
+  // operands in the epilogue instead of holding them through the main loop: held, they take the
+  // kernel past 256 VGPRs and halve its occupancy from two workgroups per CU to one (config 5's
+  // 128x128 layer-1 dgrad + addend: 118 -> 178 us).  8-wave workgroups run one per CU either way
+  // and keep the early load (its latency hides behind the main loop).
+  constexpr bool LATE = NW == 4 && TM * TN >= 16;
+  auto load_av = [&]() {
     const uint16_t* ad = (const uint16_t*)(BNB ? a.bn_x : a.addend);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -188,7 +194,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
         if constexpr (BNB) bmk[j][i] = a.bn_mask[(o + 16 * j) >> 3];
       }
     }
-  }
+  };
+  if constexpr ((ACC || BNB) && !LATE) load_av();
 
   // ---- per-lane DMA offsets (fixed for the whole kernel; chunk / tap parts are scalar)
   constexpr uint32_t kOOB = 0x80000000u;
@@ -354,6 +361,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   size_t opix[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) opix[i] = out_off(i);
+  if constexpr ((ACC || BNB) && LATE) load_av();
   if constexpr (ACC) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
