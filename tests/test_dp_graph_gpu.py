@@ -1,92 +1,21 @@
 """Graph-captured data parallelism (sqr.dist.GraphDataParallel) on one GPU: an RCCL process group
 of world size 1 (the all-reduce runs, as an identity) — gradients land in the flat buffer, the
 eager step equals plain training bitwise, and the whole step including the RCCL all-reduce is
-captured and replayed as one HIP graph with the same parameter trajectory."""
-import gc
+captured and replayed as one HIP graph with the same parameter trajectory.
 
-import numpy as np
+The checks run in a child process (tests/_dp_graph_child.py) that exits without destroying the
+communicator: that teardown, after collectives were captured in a graph, aborts intermittently
+inside RCCL on this image and would take the whole test session down with it."""
+import os
+import subprocess
+import sys
+
 import pytest
-import torch
-import torch.distributed as tdist
 
 pytestmark = pytest.mark.gpu
-DEV = "cuda:0"
-
-
-def _setup(seed=0):
-    import classes
-    import models
-    from sqr import optim as sopt
-    torch.manual_seed(seed)
-    net = models.ResNetSQ(outputs=4, pretrained=False).to(DEV)
-    opt = sopt.Adam(net.parameters(), lr=1e-3).attach(net)
-    crit = classes.ImplicitLoss(32, DEV, 1.5, 260)
-    return net, opt, crit
-
-
-def _body(net, opt, crit, x, gdp=None):
-    with torch.autocast("cuda", dtype=torch.bfloat16):
-        out = net(x)
-    loss = crit(x, torch.cat([o.float() for o in out], 1))
-    loss.backward()
-    if gdp is not None:
-        gdp.allreduce()
-    opt.step()
-    return loss.detach()
 
 
 def test_graph_dp_world1(tmp_path):
-    import classes
-    from sqr import dist as sdist
-    from sqr import gradbuf, losses
-    tdist.init_process_group("nccl", init_method="file://%s" % (tmp_path / "store"), rank=0, world_size=1,
-                             device_id=torch.device(DEV))
-    g = gdp = static = None
-    try:
-        rng = np.random.default_rng(0)
-        p = torch.tensor(classes.sample_sq_params(rng, 8), device=DEV)
-        x = losses.implicit_render(p, 256, 1.5, 260).unsqueeze(1).contiguous()
-        a_net, a_opt, a_crit = _setup()
-        b_net, b_opt, b_crit = _setup()
-        gdp = sdist.GraphDataParallel(b_net, b_opt, DEV)
-        for _ in range(2):
-            a_opt.zero_grad(set_to_none=True)
-            b_opt.zero_grad(set_to_none=True)
-            la = _body(a_net, a_opt, a_crit, x)
-            lb = _body(b_net, b_opt, b_crit, x, gdp)
-            gdp.check_grads()
-            assert torch.equal(la, lb)
-        for pa, pb in zip(a_net.parameters(), b_net.parameters()):
-            assert torch.equal(pa, pb)
-        # capture the DP step (all-reduce included) and replay it
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        torch.cuda.current_stream().wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        b_opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(g):
-            static = _body(b_net, b_opt, b_crit, x, gdp)
-        for _ in range(2):
-            g.replay()
-            a_opt.zero_grad(set_to_none=True)
-            la = _body(a_net, a_opt, a_crit, x)
-            torch.cuda.synchronize()
-            assert abs(la.item() - static.item()) <= 1e-6 * abs(la.item())
-        for pa, pb in zip(a_net.parameters(), b_net.parameters()):
-            assert (pa - pb).abs().max().item() <= 1e-5 * max(pa.abs().max().item(), 1e-3)
-    finally:
-        # teardown order: drain the device, free the captured graph (it holds RCCL work) and every
-        # object that references its memory pool, then the communicator (a destroy with live
-        # captured collectives can abort inside RCCL)
-        torch.cuda.synchronize()
-        if gdp is not None:
-            gdp.close(b_opt)
-        gradbuf.clear()
-        if g is not None:
-            g.reset()
-        del g, static, gdp
-        gc.collect()
-        torch.cuda.synchronize()
-        tdist.barrier()
-        torch.cuda.synchronize()
-        tdist.destroy_process_group()
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_dp_graph_child.py")
+    r = subprocess.run([sys.executable, "-u", child, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DP_GRAPH_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
