@@ -62,7 +62,8 @@ class Trainer:
     """bench.py's training step (also imported by tests/test_step_gpu.py, which checks exactly this
     step's gradients against a float64 reference)."""
 
-    def __init__(self, dev, config=2, batch=64, render=0, dtype=None, graph=True, rank=0, world=1, seed=1234):
+    def __init__(self, dev, config=2, batch=64, render=0, dtype=None, graph=True, rank=0, world=1, seed=1234,
+                 dp_rehearsal=False):
         import classes
         import models
         from sqr import amp, dist
@@ -90,11 +91,12 @@ class Trainer:
         self.use_graph = graph
         self.gdp = None
         self.model = self.net
-        force_dp = os.environ.get("SQR_DP_FORCE", "0") == "1"  # N=1 rehearsal of the N>1 path (world-1 RCCL)
-        if force_dp and world == 1 and not torch.distributed.is_initialized():
+        # dp_rehearsal: the N>1 path (flat buffer, bucket hooks, captured RCCL all-reduce) at N=1 on a
+        # world-1 RCCL group
+        if dp_rehearsal and world == 1 and not torch.distributed.is_initialized():
             torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get(
                 "MASTER_PORT", "29517"), rank=0, world_size=1, device_id=dev)
-        if (world > 1 or force_dp) and graph and os.environ.get("SQR_DP_GRAPH", "1") == "1":
+        if (world > 1 or dp_rehearsal) and graph:
             self.gdp = dist.GraphDataParallel(self.net, self.opt, dev)
         elif world > 1:
             self.model = dist.wrap(self.net, dev)
@@ -180,6 +182,17 @@ class Trainer:
 
     def step(self):
         return self._step()
+
+    def close(self):
+        """Release the data-parallel hooks / flat buffer; returns the graphs to destroy (before the
+        process group: sqr.dist.finish)."""
+        if self.gdp is not None:
+            self.gdp.close(self.opt)
+            self.gdp = None
+        g, self.graph = self.graph, None
+        self._step = self.eager_step
+        self.static_loss = None
+        return (g,) if g is not None else ()
 
     def probe_key(self):
         ph = PROBE[2] * self.H // 256  # layer1 runs at H/4 x H/4
@@ -268,33 +281,57 @@ def cpu_model():
 def cpu_baseline(images_cpu, params_cpu, state_dict, R, steps, cfg1_steps):
     """The reference's algorithm (oracle/ref_torch.py: stock torch CPU ops, f64 losses, Adam) timed
     on this host: config 2's workload (ImplicitLoss(R), the same batch) and config 1 (ExplicitLoss(32)
-    on the labels, B=4, fp32 network)."""
+    on the labels, B=4, fp32 network).  Thread count: BASELINE.md plans os.cpu_count(); the GPU box
+    exposes the whole machine's CPUs but runs this job on a share of them, so one timed step per
+    candidate count (16, 32, 64, ..., os.cpu_count()) picks the fastest, and every candidate's rate is
+    reported (thread_sweep) beside host_cpus."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ref_torch
-    threads = torch.get_num_threads()
+    ncpu = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = ncpu
+    cands = sorted({t for t in (16, 32, 64, 128, ncpu) if t <= ncpu} | {min(affinity, ncpu)})
 
-    def run(crit, imgs, labels, n):
+    def make():
         net = ref_torch.ResNetSQRef()
         missing = net.load_state_dict(state_dict, strict=False)
         assert not missing.missing_keys, missing.missing_keys
-        opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-        ref_torch.train_step(net, opt, crit, imgs, labels)  # warm-up
+        return net, torch.optim.Adam(net.parameters(), lr=1e-4)
+
+    def timed(net, opt, crit, imgs, labels, n):
         t0 = time.perf_counter()
         for _ in range(n):
             ref_torch.train_step(net, opt, crit, imgs, labels)
-        return imgs.shape[0] * n / (time.perf_counter() - t0), time.perf_counter() - t0
+        secs = time.perf_counter() - t0
+        return imgs.shape[0] * n / secs, secs
 
-    v, secs = run(ref_torch.ImplicitLossRef(R, 1.5, 260), images_cpu, None, steps)
-    out = {"value": v, "unit": "images/s", "cores": threads, "kind": "port",
-           "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
-           "sample": "%d train steps (1 warm-up) of batch %d: oracle/ref_torch.py ResNetSQ fp32 + "
-                     "reference-style f64 ImplicitLoss(R=%d), Adam, %d torch threads; %.1f s"
-                     % (steps, images_cpu.shape[0], R, threads, secs)}
+    crit2 = ref_torch.ImplicitLossRef(R, 1.5, 260)
+    net, opt = make()
+    ref_torch.train_step(net, opt, crit2, images_cpu, None)  # warm-up
+    sweep = {}
+    for t in cands:
+        torch.set_num_threads(t)
+        sweep[t] = timed(net, opt, crit2, images_cpu, None, 1)[0]
+    best = max(sweep, key=sweep.get)
+    torch.set_num_threads(best)
+    v, secs = timed(net, opt, crit2, images_cpu, None, steps)
+    out = {"value": v, "unit": "images/s", "cores": best, "kind": "port",
+           "host_cpus": ncpu, "affinity_cpus": affinity, "cpu_model": cpu_model(),
+           "thread_sweep": {str(k): round(x, 2) for k, x in sweep.items()},
+           "sample": "%d timed train steps of batch %d after a warm-up step and a one-step thread sweep: "
+                     "oracle/ref_torch.py ResNetSQ fp32 + reference-style f64 ImplicitLoss(R=%d), Adam, "
+                     "%d torch threads (fastest of the sweep); %.1f s" % (steps, images_cpu.shape[0], R, best, secs)}
     if cfg1_steps > 0:
-        v1, s1 = run(ref_torch.ExplicitLossRef(32), images_cpu[:4], params_cpu[:4], cfg1_steps)
-        out["config1"] = {"value": v1, "unit": "images/s",
-                          "sample": "BASELINE config 1: %d train steps (1 warm-up) of batch 4, ResNetSQ fp32 + "
-                                    "f64 ExplicitLoss(32) on the labels, Adam; %.1f s" % (cfg1_steps, s1)}
+        net, opt = make()
+        crit1 = ref_torch.ExplicitLossRef(32)
+        ref_torch.train_step(net, opt, crit1, images_cpu[:4], params_cpu[:4])  # warm-up
+        v1, s1 = timed(net, opt, crit1, images_cpu[:4], params_cpu[:4], cfg1_steps)
+        out["config1"] = {"value": v1, "unit": "images/s", "cores": best,
+                          "sample": "BASELINE config 1: %d timed train steps (after 1 warm-up) of batch 4, ResNetSQ "
+                                    "fp32 + f64 ExplicitLoss(32) on the labels, Adam, %d threads; %.1f s"
+                                    % (cfg1_steps, best, s1)}
     return out
 
 
@@ -307,11 +344,13 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config (module doc)")
     ap.add_argument("--render", type=int, default=0, help="ImplicitLoss render size R (0 = the config's)")
     ap.add_argument("--dtype", default="", choices=("", "bf16", "fp16"), help="compute dtype (default: the config's)")
-    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (0 = skip)")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-baseline steps (0 = skip)")
     ap.add_argument("--cpu1-steps", type=int, default=5, help="timed config-1 CPU steps (0 = skip)")
     ap.add_argument("--profile", action="store_true",
                     help="rocprof mode: nothing runs after the timed region (no probe / loss timing / CPU "
                          "baseline), so the last --steps step graphs of the trace are the timed ones")
+    ap.add_argument("--dp-rehearsal", action="store_true",
+                    help="N=1 only: run the data-parallel machinery (captured RCCL all-reduce) on a world-1 group")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole train step in a HIP graph (1/0; default: on)")
     args = ap.parse_args()
@@ -325,7 +364,7 @@ def main():
     rank, world, dev = dist.init("nccl")
     dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype)
     tr = Trainer(dev, config=args.config, batch=args.batch, render=args.render, dtype=dtype,
-                 graph=args.graph != 0, rank=rank, world=world)
+                 graph=args.graph != 0, rank=rank, world=world, dp_rehearsal=args.dp_rehearsal)
     B, H, R = tr.B, tr.H, tr.R
     probe_clock = None
     if tr.use_graph and not args.profile:
@@ -333,18 +372,15 @@ def main():
         _clock_reset(probe_clock)
     tr.capture(probe_clock)
 
-    def barrier():
-        dist.barrier()
-        torch.cuda.synchronize()
-
+    # dist.barrier: every rank's GPU work drained, then a host (gloo) barrier — no eager collective
+    # ever runs on the RCCL communicator that the captured step's all-reduces use
     for _ in range(args.warmup):
         tr.step()
-    barrier()
-    barrier()
+    dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = tr.step()
-    barrier()
+    dist.barrier()
     dt = time.perf_counter() - t0
     dt = dist.max_over_ranks(dt)
     final_loss = loss.item()
@@ -420,7 +456,9 @@ def main():
                                                args.cpu_steps, args.cpu1_steps)
     if rank == 0:
         os.write(json_fd, (json.dumps(out) + "\n").encode())
-    dist.finish()
+    # ordered teardown (sqr.dist.finish): the step graph with its captured all-reduces goes before
+    # the communicator
+    dist.finish(*tr.close())
 
 
 if __name__ == "__main__":

@@ -380,12 +380,17 @@ int sqr_adam_step(const sqr_adam_param* params, int nparams, double lr, double b
  * graph-capturable device steps around a backward of `loss * (*loss_scale)`:
  *   sqr_amp_check_finite  found_inf |= any non-finite element in the gradients (host arrays of device
  *                         pointers / sizes; *found_inf must be 0 before the first call of a step);
+ *   sqr_amp_check_finite_scaled  the same on the values the fused Adam will use, g * grad_scale *
+ *                         fp32(1 / *loss_scale) (loss_scale nullable): torch checks after unscaling, so a
+ *                         finite g that overflows once multiplied (scale backed off below 1) counts;
  *   sqr_adam_step_amp     sqr_adam_step on gradients g / (*loss_scale) that does nothing at all (no
  *                         update, no step-counter increment, no packing) when *found_inf != 0;
  *   sqr_amp_update_scale  GradScaler.update(): *found_inf ? scale *= backoff, tracker = 0
  *                         : ++tracker == interval ? scale *= growth, tracker = 0; then *found_inf = 0.
  * loss_scale f32, found_inf / growth_tracker int32, all device pointers. */
 int sqr_amp_check_finite(const float* const* grads, const long long* sizes, int n, int* found_inf, void* stream);
+int sqr_amp_check_finite_scaled(const float* const* grads, const long long* sizes, int n, const float* loss_scale,
+                                double grad_scale, int* found_inf, void* stream);
 int sqr_adam_step_amp(const sqr_adam_param* params, int nparams, double lr, double beta1, double beta2, double eps,
                       double grad_scale, const float* loss_scale, const int* found_inf, void* stream);
 int sqr_amp_update_scale(float* loss_scale, int* growth_tracker, int* found_inf, float growth_factor,

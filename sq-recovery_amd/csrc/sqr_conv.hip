@@ -936,8 +936,7 @@ const int kNtBN[8] = {128, 64, 128, 64, 128, 128, 128, 64};
 const int kNtThreads[8] = {256, 256, 256, 256, 512, 512, 256, 512};
 
 int nt_pick(int M, int N, bool bf16) {
-  int cfg = nt_cfg(M, N, bf16);
-  if (const char* e = getenv("SQR_NT_CFG")) cfg = atoi(e);  // experiments: force a tile config
+  const int cfg = nt_cfg(M, N, bf16);
   return cfg < 0 || cfg > 7 ? 0 : cfg;
 }
 

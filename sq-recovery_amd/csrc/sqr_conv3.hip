@@ -23,14 +23,6 @@
 #include <type_traits>
 #include "sqr_conv_dev.h"
 
-#ifndef SQR_EXP
-#define SQR_EXP 0  // timing experiments only (1: no slab stores, 2: no DMA in the loop;
-                   // conv3_kernel: 4 no per-tap wait/barrier, 8 no MFMA, 16 no fragment reads;
-                   // conv3p_kernel: 128 no MFMAs, 256 no output stores, 512 no row loads in
-                   // the tile loop; conv3s2_dgrad_kernel: 2048 no dX
-                   // stores, 4096 no MFMA, 8192 no weight loads after the prologue)
-#endif
-
 namespace sqr {
 namespace conv {
 
@@ -305,28 +297,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         V8<T> pf[TN], qf[TM];
-#if SQR_EXP & 16
-#pragma unroll
-        for (int j = 0; j < TN; ++j) pf[j] = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)poff[j], 0u, 0u, (uint32_t)sub});
-#pragma unroll
-        for (int i = 0; i < TM; ++i) qf[i] = __builtin_bit_cast(V8<T>, u32x4{(uint32_t)qoff[i], 0u, 0u, 0u});
-#else
 #pragma unroll
         for (int j = 0; j < TN; ++j) pf[j] = *(const V8<T>*)(bst + (poff[j] ^ (sub << 6)));
 #pragma unroll
         for (int i = 0; i < TM; ++i) qf[i] = *(const V8<T>*)(win + (qoff[i] ^ (sub << 6)));
-#endif
-#if SQR_EXP & 8
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM; ++i) acc[j][i][0] += __builtin_bit_cast(float, (uint32_t)(__builtin_bit_cast(u32x4, pf[j])[0] ^ __builtin_bit_cast(u32x4, qf[i])[0]));
-#else
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
-#endif
       }
       if constexpr (PD == 2) {
         const bool more = t < 7 || next;
@@ -589,10 +567,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
           bs2[2 * e + 1] = fmaf(g1, hi2f<T>(av[q][e]) - bmu[2 * e + 1], bs2[2 * e + 1]);
         }
       }
-#if SQR_EXP & 256
-      if (v[0] == 0x12345678u && v[1] == 0x9abcdef0u)
-#endif
-        __builtin_amdgcn_raw_buffer_store_b128(v, osrd, dst | (uint32_t)(c * 16), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, osrd, dst | (uint32_t)(c * 16), 0, 0);
     }
   };
   auto store_staged = [&](int k, bool use) {
@@ -670,16 +645,14 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int s = 0; s < PD; ++s) load(s, qf[s]);
 #pragma unroll
     for (int s = 0; s < NSTEP; ++s) {
-      if (s % 8 == 1 && s / 8 < NST) store_piece(k - 1, k >= 1 && !(SQR_EXP & 256), s / 8);
+      if (s % 8 == 1 && s / 8 < NST) store_piece(k - 1, k >= 1, s / 8);
       if (s % 7 == 3 && s / 7 < RPW)
-        load_row_piece(hb + 2 * (k + 2) + 1, s / 7, rvb[P], k + 2 < ntile && !(SQR_EXP & 512));
+        load_row_piece(hb + 2 * (k + 2) + 1, s / 7, rvb[P], k + 2 < ntile);
       if constexpr (ACC || BNB)
         if (s % 8 == 5 && s / 8 < NST) load_addend_piece(k, s / 8);
       if (s + PD < NSTEP) load(s + PD, qf[(s + PD) % (PD + 1)]);
-#if !(SQR_EXP & 128)
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[i] = mfma32(wreg[s], qf[s % (PD + 1)][i], acc[i]);
-#endif
 #pragma unroll
       for (int g = 0; g < TM; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // a fragment read
@@ -861,9 +834,6 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
       vo[i] = (uint32_t)(((size_t)a.cls_off[cl] + ((size_t)wrow[i] * nt + tt) * a.K + cc * 64) * 2 +
                          ((pslot ^ d3key(rr)) << 4));
     }
-#if SQR_EXP & 8192
-    if (q >= PD) return;
-#endif
     dma_pieces<PB, NW>(wsrd, bring + (q % STAGES) * TILE_B, vo, 0, wave);
   };
 #pragma unroll
@@ -926,11 +896,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-#if SQR_EXP & 4096
-              acc[cl][j][i][0] += (float)pf[j][0] * (float)qf[i][0];
-#else
               acc[cl][j][i] = mfma(pf[j], qf[i], acc[cl][j][i]);
-#endif
             }
         }
         // weight tile q+1 landed (tiles q+2 .. q+PD stay in flight; so does the next window while
@@ -992,9 +958,6 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
         for (int j = 0; j < TN; ++j) {
           const int n = wn * WN + 16 * j + 4 * fq;
           const int slot = (n >> 3) ^ ((p >> 1) & 7);
-#if SQR_EXP & 2048
-          if (acc[2 * ph + pw][j][i][0] == 1.2345f)
-#endif
           store4((T*)(smem + p * (BN * 2) + slot * 16 + (n & 4) * 2), acc[2 * ph + pw][j][i]);
         }
       }
@@ -1015,9 +978,6 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
           for (int e = 0; e < 4; ++e)
             vv[e] = pack2<T>(lo2f<T>(vv[e]) + lo2f<T>(aa[e]), hi2f<T>(vv[e]) + hi2f<T>(aa[e]));
         }
-#if SQR_EXP & 2048
-        if (v.x == 12345u)
-#endif
         *(uint4*)(out + go) = v;
       }
     }
@@ -1303,12 +1263,10 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
         __builtin_amdgcn_s_barrier();
         plan(ch0 + q + STAGES - 1);
       }
-#if !(SQR_EXP & 2)
       if constexpr (j >= 1 && j <= PER) {
         constexpr int i = j - 1, DST = (ST + STAGES - 1) % STAGES;
         if (more) piece(std::integral_constant<int, i>{}, DST);
       }
-#endif
       if constexpr (j + D < NS) {
         issue(stc, std::integral_constant<int, j + D>{});
       } else if constexpr (!LAST) {
@@ -1352,21 +1310,12 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   const size_t ng = (size_t)9 * a.C;
   float* __restrict__ slab = a.slab + (size_t)split * a.K * ng;
   const int c = c0 + 16 * wave + 4 * fq;
-#if SQR_EXP & 1
-  float sum = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) sum += acc[t][kt][0] + acc[t][kt][1] + acc[t][kt][2] + acc[t][kt][3];
-  if (sum == 1234.5f) slab[tid] = sum;
-#else
 #pragma unroll
   for (int kt = 0; kt < 4; ++kt) {
     float* row = slab + (size_t)(k0 + 16 * kt + fr) * ng + c;
 #pragma unroll
     for (int t = 0; t < 9; ++t) *(f32x4*)(row + t * a.C) = acc[t][kt];
   }
-#endif
   clock_end(a.tp);
 }
 
@@ -1404,10 +1353,7 @@ bool pick(int N, int H, int W, int Cin, int Nout, D3Cfg* out) {
       {4, 256, 64, 256, 16, 16, 2, 1},   // W 16, whole image per tile (slower than id 2 on layer3)
       {6, 256, 32, 256, 8, 8, 2, 4},     // 8 x 8, four images per tile
   };
-  int force = -1;
-  if (const char* e = getenv("SQR_D3_CFG")) force = atoi(e);  // experiments: force a configuration
   for (const D3Cfg& c : cands) {
-    if (force >= 0 && c.id != force) continue;
     if (c.id == 0 && !(Nout == 64 && nch == 1)) continue;
     if (c.id != 0 && Nout % c.BN) continue;
     if (W % c.TW || H % c.TH) continue;

@@ -361,11 +361,15 @@ struct FJobs {
   int start[MAXF + 1];  // first workgroup of each tensor
   int nj;
   int* found_inf;
+  const float* loss_scale;  // nullable: values are checked as g * gscale * fp32(1 / *loss_scale)
+  float gscale;             //   (exactly the multiplier sqr_adam_step_amp applies)
 };
 constexpr int FCHUNK = 16384;  // elements per workgroup
 
-// found_inf |= any(!isfinite(g)) over every tensor (GradScaler's unscale_ check; the unscale
-// multiply itself is folded into the Adam kernel)
+// found_inf |= any(!isfinite(g * m)) over every tensor, m = the unscale multiplier the fused Adam
+// applies (GradScaler's unscale_ check on the unscaled values, as torch's
+// _amp_foreach_non_finite_check_and_unscale_: a finite g can overflow once multiplied by 1 / scale
+// when the scale has backed off below 1); m = 1 without a loss scale
 __global__ void __launch_bounds__(256) amp_check_kernel(FJobs J) {
   const int b = blockIdx.x;
   int ji = 0;
@@ -373,17 +377,19 @@ __global__ void __launch_bounds__(256) amp_check_kernel(FJobs J) {
   const long long i0 = (long long)(b - J.start[ji]) * FCHUNK;
   const long long i1 = i0 + FCHUNK < J.n[ji] ? i0 + FCHUNK : J.n[ji];
   const float* g = J.g[ji];
+  const float m = J.loss_scale ? J.gscale * (float)(1.0 / (double)*J.loss_scale) : J.gscale;
+  // x - x is NaN for inf and NaN inputs, 0 otherwise (no isfinite on the vector path)
+  auto bad1 = [&](float x) { x = m == 1.f ? x : x * m; return !((x - x) == 0.f); };
   bool bad = false;
   if (((uintptr_t)g & 15) == 0) {
     const long long v1 = i0 + ((i1 - i0) & ~3ll);
     for (long long i = i0 + 4 * threadIdx.x; i < v1; i += 4 * 256) {
       const f32x4 v = *(const f32x4*)(g + i);
-      // x - x is NaN for inf and NaN inputs, 0 otherwise (no isfinite on the vector path)
-      bad |= !((v[0] - v[0]) == 0.f) | !((v[1] - v[1]) == 0.f) | !((v[2] - v[2]) == 0.f) | !((v[3] - v[3]) == 0.f);
+      bad = bad || bad1(v[0]) || bad1(v[1]) || bad1(v[2]) || bad1(v[3]);
     }
-    for (long long i = v1 + threadIdx.x; i < i1; i += 256) bad |= !((g[i] - g[i]) == 0.f);
+    for (long long i = v1 + threadIdx.x; i < i1; i += 256) bad |= bad1(g[i]);
   } else {
-    for (long long i = i0 + threadIdx.x; i < i1; i += 256) bad |= !((g[i] - g[i]) == 0.f);
+    for (long long i = i0 + threadIdx.x; i < i1; i += 256) bad |= bad1(g[i]);
   }
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(J.found_inf, 1);
 }
@@ -413,14 +419,16 @@ __global__ void amp_update_kernel(float* scale, int* tracker, int* found_inf, fl
 }  // namespace optim
 }  // namespace sqr
 
-extern "C" int sqr_amp_check_finite(const float* const* grads, const long long* sizes, int n, int* found_inf,
-                                    void* stream) {
+extern "C" int sqr_amp_check_finite_scaled(const float* const* grads, const long long* sizes, int n,
+                                           const float* loss_scale, double grad_scale, int* found_inf, void* stream) {
   SQR_CHECK_ARG(grads && sizes && found_inf && n >= 0, "amp_check_finite: null argument");
   hipStream_t st = as_stream(stream);
   for (int i0 = 0; i0 < n; i0 += MAXF) {
     FJobs J;
     J.nj = 0;
     J.found_inf = found_inf;
+    J.loss_scale = loss_scale;
+    J.gscale = (float)grad_scale;
     int blocks = 0;
     for (int i = i0; i < n && i < i0 + MAXF; ++i) {
       SQR_CHECK_ARG(grads[i] && sizes[i] > 0, "amp_check_finite: tensor %d: null pointer or empty", i);
@@ -436,6 +444,11 @@ extern "C" int sqr_amp_check_finite(const float* const* grads, const long long* 
     SQR_HIP_LAUNCH_CHECK("amp_check_kernel");
   }
   return 0;
+}
+
+extern "C" int sqr_amp_check_finite(const float* const* grads, const long long* sizes, int n, int* found_inf,
+                                    void* stream) {
+  return sqr_amp_check_finite_scaled(grads, sizes, n, nullptr, 1.0, found_inf, stream);
 }
 
 extern "C" int sqr_amp_update_scale(float* scale, int* growth_tracker, int* found_inf, float growth_factor,

@@ -509,11 +509,7 @@ extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a,
   SQR_CHECK_ARG(x && out_a && out_e && out_t && out_q && save, "tail_fwd: null pointer");
   const Dev d = make_dev(t, x);
   hipStream_t st = as_stream(stream);
-  static const int split = [] {
-    const char* e = getenv("SQR_TAIL_SPLIT");
-    return e ? atoi(e) : 1;
-  }();
-  if (split && t->F1 % 16 == 0 && t->F2 % 16 == 0) {  // three launches, 4 workgroups per sample in fc0 / fc1
+  if (t->F1 % 16 == 0 && t->F2 % 16 == 0) {  // three launches, 4 workgroups per sample in fc0 / fc1
     if (t->dtype == SQR_DTYPE_BF16)
       hipLaunchKernelGGL(tail_fc0_kernel<bf16>, dim3(t->B, 4), dim3(256), 0, st, d, save);
     else if (t->dtype == SQR_DTYPE_F16)

@@ -40,10 +40,14 @@ def _unwrap(model):
     return model.module if hasattr(model, "module") and isinstance(model.module, torch.nn.Module) else model
 
 
-def save_model(path, epoch, model, optimizer, loss):
-    """helpers.py:42-48."""
-    torch.save({"epoch": epoch, "model_state_dict": _unwrap(model).state_dict(),
-                "optimizer_state_dict": optimizer.state_dict(), "loss": loss}, path)
+def save_model(path, epoch, model, optimizer, loss, scaler=None):
+    """helpers.py:42-48.  scaler (optional, fp16 runs): its state_dict goes under the extra key
+    'scaler_state_dict' — the reference's four keys are unchanged, so either side loads the file."""
+    ck = {"epoch": epoch, "model_state_dict": _unwrap(model).state_dict(),
+          "optimizer_state_dict": optimizer.state_dict(), "loss": loss}
+    if scaler is not None:
+        ck["scaler_state_dict"] = scaler.state_dict()
+    torch.save(ck, path)
 
 
 def _safe_load(path, map_location):
@@ -56,14 +60,18 @@ def _safe_load(path, map_location):
             return torch.load(path, map_location=map_location, weights_only=True)
 
 
-def load_model(path, model, optimizer, plot=False):
-    """helpers.py:51-68 (map_location cuda:0 when a GPU is present, as the reference)."""
+def load_model(path, model, optimizer, plot=False, scaler=None):
+    """helpers.py:51-68 (map_location cuda:0 when a GPU is present, as the reference).  scaler
+    (optional): restored from 'scaler_state_dict' when the checkpoint has it (a resumed fp16 run
+    keeps its loss scale and growth tracker)."""
     print("Loading model: " + path)
     dev = "cuda:0" if torch.cuda.is_available() else "cpu"
     checkpoint = _safe_load(path, dev)
     _unwrap(model).load_state_dict(checkpoint["model_state_dict"])
     if optimizer is not None:
         optimizer.load_state_dict(checkpoint["optimizer_state_dict"])
+    if scaler is not None and "scaler_state_dict" in checkpoint:
+        scaler.load_state_dict(checkpoint["scaler_state_dict"])
     epoch = checkpoint["epoch"]
     loss = checkpoint["loss"]
     if plot:

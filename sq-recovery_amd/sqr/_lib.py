@@ -158,6 +158,8 @@ SIGNATURES = {
                                   c_double, c_void_p, c_void_p, c_void_p]),
     "sqr_amp_check_finite": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong), c_int, c_void_p,
                                      c_void_p]),
+    "sqr_amp_check_finite_scaled": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_longlong), c_int,
+                                            c_void_p, c_double, c_void_p, c_void_p]),
     "sqr_amp_update_scale": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_float, c_int, c_void_p]),
     "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

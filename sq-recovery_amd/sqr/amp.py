@@ -6,9 +6,16 @@ every piece device-resident and stream-ordered, so a whole fp16 training step â€
 backward, overflow check, (skipped or applied) Adam, scale update â€” is capturable in one HIP graph:
 
   scale(loss)   loss * scale (one kernel; the scale is a device f32)
-  step(opt)     sqr_amp_check_finite over every gradient (found_inf |= any non-finite), then
-                sqr_adam_step_amp: Adam on g / scale, or nothing at all when found_inf is set
+  step(opt)     sqr_amp_check_finite_scaled over every gradient (found_inf |= any non-finite value of
+                g * grad_scale / scale â€” checked after the multiply, as torch does), then
+                sqr_adam_step_amp: Adam on g * grad_scale / scale, or nothing at all when found_inf is set
   update()      sqr_amp_update_scale: backoff / growth of the scale, clears found_inf
+  unscale_(opt) multiplies the gradients in place by grad_scale / scale (so clipping etc. sees
+                averaged, unscaled gradients, as with torch DDP + GradScaler) and sets the optimizer's
+                grad_scale to 1 until step() / update()
+
+``grad_scale`` is the optimizer's ``sqr_grad_scale``: 1 / world under sqr.dist.GraphDataParallel,
+whose flat-buffer gradients are rank sums (the average is folded into the fused Adam).
 
 The reference trains in fp32 without a scaler (torch/train.py:50-100); torch pairs fp16 autocast
 with exactly this scaler, which is what config 5 ("fp16 + loss scaling") asks for.
@@ -49,6 +56,7 @@ class GradScaler:
         self._growth_tracker = torch.zeros((), dtype=torch.int32, device=self.device)
         self._found_inf = torch.zeros((), dtype=torch.int32, device=self.device)
         self._unscaled = set()
+        self._saved_gscale = {}  # id(optimizer) -> its sqr_grad_scale while unscale_ took it over
 
     def scale(self, outputs):
         return outputs * self._scale
@@ -63,23 +71,39 @@ class GradScaler:
                     gs.append(p.grad)
         return gs
 
-    def _check(self, optimizer):
+    def _check(self, optimizer, scaled):
+        """found_inf |= any non-finite gradient value as the optimizer will use it: g * grad_scale /
+        scale when `scaled` (step() without unscale_), else g itself (already multiplied)."""
         spans = _merged_ranges(self._grads(optimizer))
         if not spans:
             return
         n = len(spans)
         ptrs = (ctypes.c_void_p * n)(*[p for p, _ in spans])
         sizes = (ctypes.c_longlong * n)(*[s for _, s in spans])
-        check(lib().sqr_amp_check_finite(ptrs, sizes, n, ptr(self._found_inf), stream_ptr(self.device)),
-              "sqr_amp_check_finite")
+        gs = float(getattr(optimizer, "sqr_grad_scale", 1.0)) if scaled else 1.0
+        check(lib().sqr_amp_check_finite_scaled(ptrs, sizes, n, ptr(self._scale) if scaled else None, gs,
+                                                ptr(self._found_inf), stream_ptr(self.device)),
+              "sqr_amp_check_finite_scaled")
+
+    def _restore(self, optimizer=None):
+        for oid, (opt, gs) in list(self._saved_gscale.items()):
+            if optimizer is None or oid == id(optimizer):
+                opt.sqr_grad_scale = gs
+                del self._saved_gscale[oid]
 
     def unscale_(self, optimizer):
-        """Divide the gradients by the scale in place (e.g. before gradient clipping)."""
+        """Multiply the gradients in place by grad_scale / scale (e.g. before gradient clipping): they
+        are then the unscaled, rank-averaged gradients; the non-finite check runs on those values."""
         if id(optimizer) in self._unscaled:
             raise RuntimeError("unscale_() has already been called on this optimizer since the last update()")
-        self._check(optimizer)
-        inv = self._scale.double().reciprocal().float()
-        torch._foreach_mul_(self._grads(optimizer), inv)
+        gs = float(getattr(optimizer, "sqr_grad_scale", 1.0))
+        # the fused Adam's multiplier: fp32(grad_scale) * fp32(1 / scale)
+        mult = self._scale.double().reciprocal().float() * gs
+        torch._foreach_mul_(self._grads(optimizer), mult)
+        self._check(optimizer, scaled=False)
+        if hasattr(optimizer, "sqr_grad_scale"):
+            self._saved_gscale[id(optimizer)] = (optimizer, gs)
+            optimizer.sqr_grad_scale = 1.0  # folded into the gradients above, until step()/update()
         self._unscaled.add(id(optimizer))
 
     def step(self, optimizer, *args, **kw):
@@ -87,12 +111,13 @@ class GradScaler:
             raise TypeError("sqr GradScaler drives sqr.optim.Adam only")
         unscaled = id(optimizer) in self._unscaled
         if not unscaled:
-            self._check(optimizer)
+            self._check(optimizer, scaled=True)
         optimizer.sqr_amp = (None if unscaled else self._scale, self._found_inf)
         try:
             return optimizer.step(*args, **kw)
         finally:
             optimizer.sqr_amp = None
+            self._restore(optimizer)
 
     def update(self, new_scale=None):
         if new_scale is not None:
@@ -103,6 +128,7 @@ class GradScaler:
                                              ctypes.c_float(self.growth_factor), ctypes.c_float(self.backoff_factor),
                                              self.growth_interval, stream_ptr(self.device)), "sqr_amp_update_scale")
         self._unscaled.clear()
+        self._restore()
 
     def get_scale(self):
         return float(self._scale.item())

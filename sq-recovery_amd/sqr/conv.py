@@ -8,8 +8,6 @@ torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
 Compute dtype: bfloat16 / float16 when the input has that dtype or CUDA autocast is on with it,
 else float32 (exact-f32 MFMA: the parity mode).
 """
-import os
-
 import torch
 import torch.nn as nn
 
@@ -29,10 +27,6 @@ _CL = torch.channels_last
 #   clock:  rows of an int64 device tensor [n, 2] receiving the kernel's own wall-clock span
 #           (sqr_probe_arm_clock; works inside replayed graphs: the slot pointer is a kernel argument).
 _probe = {"key": None, "events": [], "clock": None, "nclock": 0}
-
-# ablation switch: SQR_BN_RIDE=0 runs a linked BatchNorm's backward finalize as its own launch
-# instead of as extra workgroups of the conv's weight-gradient reduction
-_RIDE = os.environ.get("SQR_BN_RIDE", "1") != "0"
 
 
 def set_probe(phase, N, C, H, K, R, stride, clock=None):
@@ -307,7 +301,9 @@ class BnBackwardLink:
         etc. are None unless the conv's weight-gradient launch also finalized the BatchNorm);
         clears the link."""
         got = (self.g, self.stats, self.coef, self.dgamma, self.dbeta)
+        # the link is spent: drop every tensor it holds (the forward operands too)
         self.g = self.stats = self.coef = self.dgamma = self.dbeta = None
+        self.x = self.mask = self.mean = self.invstd = self.gamma = self.pids = None
         g = got[0]
         if g is None or got[1] is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
             return None
@@ -366,7 +362,10 @@ class BnOutLink:
     def take(self, dy):
         """(part, rows) if dy is the gradient the riding reduction summed, else None; clears."""
         g, part, rows = self.g, self.part, self.rows
+        # spent: release the partials and the forward operands (the block output that carries this
+        # link as y._sqr_outlink may outlive the backward)
         self.g = self.part = self.rows = None
+        self.x_a = self.mean_a = self.x_b = self.mean_b = self.mask = None
         if g is None or part is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
             return None
         return part, rows.value
@@ -396,20 +395,32 @@ class ResidualJoin:
         return None
 
     def deposit(self, g):
-        """Branch side: the gradient to return to autograd (None when deposited)."""
+        """Branch side: the gradient to return to autograd (None when deposited).  A deposit that
+        conv1's backward never takes in the same backward pass (conv1 outside the differentiated
+        graph) would be a lost gradient: the end-of-backward check raises instead."""
         if g is None:
             return None
         if self.acc_done:  # conv1's backward already ran: autograd adds this one
             self.acc_done = False
             return g
         self.pending = g
+        if torch._C._current_graph_task_id() != -1:  # inside a backward pass (always, in the model)
+            torch.autograd.Variable._execution_engine.queue_callback(self._check_taken)
         return None
+
+    def _check_taken(self):
+        if self.pending is not None:
+            self.pending = None
+            raise RuntimeError("sqr ResidualJoin: the residual branch's gradient was deposited for conv1's "
+                               "backward-data, which did not run in this backward pass")
 
     def take(self):
         """conv1 side: the deposited gradient (or None: conv1 runs first, the branch returns its own)."""
         g, self.pending = self.pending, None
         if g is None:
             self.acc_done = True
+        else:
+            self.acc_done = False
         return g
 
 
@@ -494,11 +505,11 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             fin = None
             link = ctx.bnb
-            if _RIDE and link is not None and link.stats is not None and link.g is not None and col is None \
+            if link is not None and link.stats is not None and link.g is not None and col is None \
                     and link.pids is not None:
                 fin = link.fin_job(d.C, g.device)  # the linked BatchNorm's finalize rides this launch
             red = None
-            if _RIDE and ride_red is not None and ride_red.ready() and col is None and dx is not None \
+            if ride_red is not None and ride_red.ready() and col is None and dx is not None \
                     and dx.dtype == ride_red.x_a.dtype and dx.shape == ride_red.x_a.shape:
                 red = ride_red.red_job(dx)
             dw = conv2d_bwd_weight(xin, g, d, col, ctx.wid, fin, red)

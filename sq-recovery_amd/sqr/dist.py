@@ -7,6 +7,7 @@ collective is the gradient all-reduce, bucketed and overlapped with backward by 
 SyncBN is the documented multi-GPU semantics: an N-rank step equals the average of N independent
 per-rank gradients).  ``wrap`` (torch DDP) remains as the fallback when a step cannot be captured.
 """
+import gc
 import os
 
 import torch
@@ -24,13 +25,38 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(backend="nccl"):
+# Host-side synchronisation (barriers, timing / logging reductions) runs on a gloo group of its
+# own, never on the RCCL communicator: that communicator carries only the gradient all-reduces,
+# which bench.py captures in its step graph.  Eager RCCL collectives issued after a graph with
+# captured RCCL work was replayed or destroyed are what aborted inside RCCL in round 2 (a
+# tdist.barrier() right after CUDAGraph.reset()); with the host group the communicator sees no
+# eager work after the first capture, and its teardown (finish) follows the ordered sequence below.
+_host = [None]
+
+
+def host_group():
+    """The gloo group for host-side collectives (the default group when that is gloo already).
+    Created on first use; every rank reaches it through the same collective calls."""
+    if not dist.is_initialized():
+        return None
+    if dist.get_backend() == "gloo":
+        return dist.group.WORLD
+    if _host[0] is None:
+        _host[0] = dist.new_group(backend="gloo")
+    return _host[0]
+
+
+def init(backend="nccl", device_type=None):
     """Set this rank's device and join the process group when WORLD_SIZE > 1.
-    Returns (rank, world, device)."""
+    Returns (rank, world, device).  backend "gloo" with device_type "cuda" keeps the GPU path on a
+    gloo group (several ranks on one GPU: the multi-rank GPU tests; RCCL refuses duplicate GPUs)."""
     rank, world, local = env()
-    if backend == "nccl":
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+    device_type = device_type or ("cuda" if backend == "nccl" else "cpu")
+    if device_type == "cuda":
+        ndev = torch.cuda.device_count()
+        idx = local % ndev if ndev else local
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
@@ -38,6 +64,7 @@ def init(backend="nccl"):
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
+        host_group()
     return rank, world, device
 
 
@@ -210,30 +237,61 @@ class GraphDataParallel:
             optimizer.sqr_grad_scale = 1.0
 
 
+def capturable():
+    """Whether the gradient all-reduce can be captured in a HIP graph: RCCL (or no process group);
+    gloo all-reduces of CUDA tensors go through the host and run eagerly only."""
+    return not (dist.is_initialized() and dist.get_world_size() > 1 and dist.get_backend() != "nccl")
+
+
+def _multi():
+    return dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _cuda_live():
+    return torch.cuda.is_available() and torch.cuda.is_initialized()
+
+
 def max_over_ranks(x):
-    """max of a host float over all ranks (bench timing: the job is as slow as its slowest rank)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    """max of a host float over all ranks (bench timing: the job is as slow as its slowest rank);
+    host group (gloo)."""
+    if not _multi():
         return float(x)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=host_group())
     return t.item()
 
 
 def mean_over_ranks(x):
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not _multi():
         return float(x)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    t = torch.tensor([float(x)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=host_group())
     return t.item() / dist.get_world_size()
 
 
 def barrier():
-    if dist.is_initialized() and dist.get_world_size() > 1:
-        dist.barrier()
+    """Every rank's queued GPU work has finished, then a host barrier (gloo): the bench's timed
+    region starts and ends with all devices idle."""
+    if _cuda_live():
+        torch.cuda.synchronize()
+    if _multi():
+        dist.barrier(group=host_group())
 
 
-def finish():
+def finish(*graphs):
+    """Ordered teardown: drain the device; destroy the step graphs (the RCCL plans captured in them
+    are released with the graph, and must be before their communicator goes); drain again; wait for
+    every rank on the host group; only then destroy the process groups (RCCL communicator included)."""
+    if _cuda_live():
+        torch.cuda.synchronize()
+    for g in graphs:
+        if g is not None:
+            g.reset()
+    gc.collect()
+    if _cuda_live():
+        torch.cuda.synchronize()
     if dist.is_initialized():
+        if dist.get_world_size() > 1:
+            dist.barrier(group=host_group())
         dist.destroy_process_group()
+    _host[0] = None

@@ -16,16 +16,6 @@ from .bn import bn_act, bn_add_act, count_batches, fused_stem, fused_stem_ok, st
 from .conv import BnBackwardLink, BnOutLink, Conv2d, ResidualJoin, compute_dtype, pack_all
 
 
-# ablation switches (A/B timing in one process / on one box; both default on):
-#   SQR_RESIDUAL_JOIN=0  the residual branch's gradient goes back through autograd's add
-#   SQR_BN_ADD=0         bn2 + downsample-bn as two BatchNorm ops (the identity tensor is written)
-#   SQR_BN_LINK=0        bn1's backward reduction as its own pass (not in conv2's dgrad epilogue)
-_JOIN = os.environ.get("SQR_RESIDUAL_JOIN", "1") != "0"
-_BN_ADD = os.environ.get("SQR_BN_ADD", "1") != "0"
-_BN_LINK = os.environ.get("SQR_BN_LINK", "1") != "0"
-_JOIN_MAXHW = int(os.environ.get("SQR_JOIN_MAXHW", str(1 << 30)))  # experiments: largest map with the join
-
-
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -48,24 +38,19 @@ class BasicBlock(nn.Module):
         # (training: each conv's epilogue also emits the batch statistics its BN needs; backward:
         # the identity / downsample branch's gradient of x is added in conv1's backward-data
         # epilogue through a ResidualJoin instead of a separate add)
-        join = ResidualJoin.make(x) if (_JOIN and x.shape[2] * x.shape[3] <= _JOIN_MAXHW) else None
+        join = ResidualJoin.make(x)
         # bn1's backward reduction in conv2's backward-data epilogue pays off up to 64x64 maps (the
         # persistent layer-1 kernel at 256x256 input and every deeper layer); the tiled kernel on the
         # 128x128 layer-1 maps of 512x512 input runs 118 -> 212 us with it (same-box A/B of config 5:
         # +0.9 % without the link), so larger maps keep bn1's own reduction pass
         hw = (x.shape[2] // self.stride) * (x.shape[3] // self.stride)
-        link = BnBackwardLink.make(x, self.bn1) if (_BN_LINK and hw <= 64 * 64) else None
+        link = BnBackwardLink.make(x, self.bn1) if hw <= 64 * 64 else None
         # x's producer (the previous block's output BatchNorm) may have its backward reduction ride
         # on conv1's weight-gradient launch (BnOutLink)
         red_link = getattr(x, "_sqr_outlink", None) if join is not None else None
         out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc", bnr=red_link), self.bn1, relu=True,
                      counted=True, link=link)
-        out_link = BnOutLink(2 if self.downsample is not None else 1) if (join is not None and _BN_LINK) else None
-        if self.downsample is not None and not _BN_ADD:
-            identity = bn_act(self.downsample[0].forward_stats(x, self.downsample[1], join=join, role="dep"),
-                              self.downsample[1], relu=False, counted=True)
-            return bn_act(self.conv2.forward_stats(out, self.bn2, bnb=link), self.bn2, residual=identity, relu=True,
-                          counted=True)
+        out_link = BnOutLink(2 if self.downsample is not None else 1) if join is not None else None
         if self.downsample is not None:
             # bn2(conv2) + bn_ds(conv_ds) + ReLU as ONE op: the downsample branch is never normalised
             # into a tensor of its own (sqr_bn_add_*)

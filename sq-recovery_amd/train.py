@@ -20,11 +20,17 @@ MI355X-specific:
     step), each rank trains on its own contiguous shard (sqr.dist.shard), rank 0 logs and writes
     checkpoints (un-prefixed state-dict keys);
   * --synthetic N trains on N rendered SQ images (no dataset files needed); otherwise the
-    reference's H5Dataset(dataset_location, parse_csv(labels), 0.9) is used (needs h5py).
+    reference's H5Dataset(dataset_location, parse_csv(labels), 0.9) is used (needs h5py);
+  * on CUDA the whole training step (forward, loss, backward, all-reduce, Adam / loss scaler) is
+    captured in one HIP graph and replayed per batch (sqr.step.CapturedStep: static batch buffers,
+    loss and the NaN check of encoder.fc[0].weight.grad read back one step behind, so the host
+    never stalls the device); --graph 0 runs the reference's eager loop;
+  * each epoch prints its training throughput (images/s over all ranks, train loop only).
 """
 import argparse
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -39,6 +45,7 @@ from models import ResNetSQ  # noqa: E402
 from sqr import amp, dist  # noqa: E402
 from sqr.data import DevicePrefetcher  # noqa: E402
 from sqr.optim import Adam  # noqa: E402
+from sqr.step import CapturedStep  # noqa: E402
 
 
 def parse_args(argv=None):
@@ -64,6 +71,10 @@ def parse_args(argv=None):
     ap.add_argument("--compare-images", action="store_true",
                     help="render val batch 0 with the external scanner (helpers.save_compare_images)")
     ap.add_argument("--max-steps", type=int, default=0, help="stop an epoch after this many steps (0 = all)")
+    ap.add_argument("--graph", type=int, default=1, help="capture the training step in a HIP graph (CUDA; 0 = eager)")
+    ap.add_argument("--dist-backend", default="", choices=("", "nccl", "gloo"),
+                    help="process-group backend (default: nccl on CUDA, gloo on CPU; gloo on CUDA runs several "
+                         "ranks on one GPU)")
     return ap.parse_args(argv)
 
 
@@ -86,7 +97,8 @@ def _batches(dataset, rank, world, batch_size, device=torch.device("cpu")):
 def main(argv=None):
     args = parse_args(argv)
     use_cuda = args.device == "cuda" or (args.device == "auto" and torch.cuda.is_available())
-    rank, world, device = dist.init("nccl" if use_cuda else "gloo")
+    rank, world, device = dist.init(args.dist_backend or ("nccl" if use_cuda else "gloo"),
+                                    "cuda" if use_cuda else "cpu")
     main_rank = rank == 0
     if main_rank:
         print("Using device: %s (world size %d)" % (device, world))
@@ -109,7 +121,7 @@ def main(argv=None):
     if args.continue_training:
         if main_rank:
             print("Continuing with training...")
-        starting_epoch, net, optimizer, _ = load_model(args.model_location, net, optimizer)
+        starting_epoch, net, optimizer, _ = load_model(args.model_location, net, optimizer, scaler=scaler)
     # N > 1: bucketed gradient all-reduce overlapped with backward (the same machinery bench.py
     # captures in its step graph); the model itself stays unwrapped (checkpoints keep plain keys)
     gdp = dist.GraphDataParallel(net, optimizer, device) if world > 1 else None
@@ -132,6 +144,24 @@ def main(argv=None):
             out = model(x)
         return torch.cat([o.float() for o in out], dim=1)
 
+    def train_body(x, labels):
+        pred_labels = forward(x)
+        loss = loss_criterion(x, labels, pred_labels)
+        (scaler.scale(loss) if scaler is not None else loss).backward()
+        if gdp is not None:
+            gdp.allreduce()
+        if scaler is not None:
+            scaler.step(optimizer)
+            scaler.update()
+        else:
+            optimizer.step()
+        return loss
+
+    # the reference's per-step NaN check (train.py:115) on encoder.fc[0].weight.grad
+    # (a gloo process group on CUDA — several ranks on one GPU — all-reduces through the host: eager)
+    stepper = CapturedStep(train_body, optimizer, device, check=lambda: net.encoder.fc[0].weight.grad,
+                           graph=bool(args.graph) and dist.capturable())
+
     best_val_loss = None
     mean_losses, mean_val_losses, mean_val_accs = [], [], []
     for epoch in range(starting_epoch, args.epochs):
@@ -139,29 +169,39 @@ def main(argv=None):
         net.train()
         dataset.set_mode(0)
         n_items = len(dataset)
+        sizes = []
+
+        def report(results):
+            # (loss, nan) of finished steps in order: the reference's bookkeeping and log lines
+            for loss_v, nan in results:
+                step_idx = len(losses)
+                losses.append(loss_v)
+                if nan:
+                    print("--------------- NAN GRADS!!!! ---------------")
+                if main_rank and step_idx % args.log_interval == 0:
+                    sys.stdout.write("\033[K")
+                    print("Train Epoch: {} Step: {} [{}/{}]\tLoss: {:,.6f}".format(
+                        epoch, step_idx, (step_idx + 1) * sizes[step_idx] * world, n_items,
+                        np.mean(losses[-args.running_mean:])), end="\r")
+
+        dist.barrier()
+        t0 = time.perf_counter()
         for batch_idx, (x, true_labels) in enumerate(_batches(dataset, rank, world, args.batch_size, device)):
             if args.max_steps and batch_idx >= args.max_steps:
                 break
             x, true_labels = x.to(device, non_blocking=True), true_labels.to(device, non_blocking=True)
-            optimizer.zero_grad(set_to_none=True)
-            pred_labels = forward(x)
-            loss = loss_criterion(x, true_labels, pred_labels)
-            (scaler.scale(loss) if scaler is not None else loss).backward()
-            if gdp is not None:
-                gdp.allreduce()
-            if scaler is not None:
-                scaler.step(optimizer)
-                scaler.update()
-            else:
-                optimizer.step()
-            losses.append(loss.item())
-            if torch.any(torch.isnan(net.encoder.fc[0].weight.grad)):
-                print("--------------- NAN GRADS!!!! ---------------")
-            if main_rank and batch_idx % args.log_interval == 0:
-                sys.stdout.write("\033[K")
-                print("Train Epoch: {} Step: {} [{}/{}]\tLoss: {:,.6f}".format(
-                    epoch, batch_idx, (batch_idx + 1) * len(x) * world, n_items,
-                    np.mean(losses[-args.running_mean:])), end="\r")
+            sizes.append(len(x))
+            stepper.step(x, true_labels)
+            # log one step behind: the previous step has finished by the time this one is queued
+            report(stepper.drain(stepper.launched - 1 if stepper.graph is not None else None))
+        report(stepper.drain())
+        dist.barrier()
+        secs = dist.max_over_ranks(time.perf_counter() - t0)
+        if main_rank and losses:
+            sys.stdout.write("\033[K")
+            print("Train Epoch: {} throughput: {:.1f} images/s ({} steps, {} ranks, {})".format(
+                epoch, sum(sizes) * world / secs, len(sizes), world,
+                "HIP graph" if stepper.captures else "eager"))
         train_mean = dist.mean_over_ranks(np.mean(losses)) if losses else float("nan")
         mean_losses.append(train_mean)
         if main_rank:
@@ -195,7 +235,8 @@ def main(argv=None):
                 best_val_loss = val_loss_mean
                 os.makedirs(os.path.dirname(args.model_location) or ".", exist_ok=True)
                 save_model(args.model_location, epoch, model, optimizer,
-                           {"loss": mean_losses, "val_loss": mean_val_losses, "val_acc": mean_val_accs})
+                           {"loss": mean_losses, "val_loss": mean_val_losses, "val_acc": mean_val_accs},
+                           scaler=scaler)
             print("-" * 72)
             print("Validation Epoch: {}\tLoss: {:,.6f}\tAccuracy: {:,.6f}".format(epoch, val_loss_mean,
                                                                                  val_accuracy_mean))
@@ -204,7 +245,8 @@ def main(argv=None):
             best_val_loss = val_loss_mean if best_val_loss is None else min(best_val_loss, val_loss_mean)
     if gdp is not None:
         gdp.close(optimizer)
-    dist.finish()
+    # ordered teardown: the step graph (with any captured all-reduces) before the process group
+    dist.finish(stepper.close())
     return mean_losses, mean_val_losses
 
 

@@ -1,7 +1,8 @@
 """Child process of tests/test_dp_graph_gpu.py: the graph-captured data-parallel step on a world-1
-RCCL group.  Prints DP_GRAPH_OK once every check passed and leaves with os._exit(0): destroying a
-communicator whose collectives were captured in a HIP graph aborts intermittently inside RCCL on
-this image, so the process never runs that teardown (the driver reclaims everything at exit)."""
+RCCL group, then the product teardown (sqr.dist.finish: drain, destroy the step graph with its
+captured all-reduces, host barrier, destroy the process groups) and a normal interpreter exit.
+Prints DP_GRAPH_OK after every check passed and DP_TEARDOWN_OK after destroy_process_group returned;
+the parent also requires exit status 0 (an abort during teardown or at exit fails the test)."""
 import os
 import sys
 
@@ -79,14 +80,19 @@ def run(tmp_path):
             assert abs(la.item() - static.item()) <= 1e-6 * abs(la.item())
         for pa, pb in zip(a_net.parameters(), b_net.parameters()):
             assert (pa - pb).abs().max().item() <= 1e-5 * max(pa.abs().max().item(), 1e-3)
+        print("DP_GRAPH_OK", flush=True)
     finally:
-        torch.cuda.synchronize()
+        if gdp is not None:
+            gdp.close(b_opt)
         gradbuf.clear()
+        static = None
+        # the same ordered teardown bench.py / train.py use
+        sdist.finish(g)
+        g = None
+        assert not tdist.is_initialized()
+        print("DP_TEARDOWN_OK", flush=True)
 
 
 if __name__ == "__main__":
     import pathlib
     run(pathlib.Path(sys.argv[1]))
-    print("DP_GRAPH_OK", flush=True)
-    sys.stdout.flush()
-    os._exit(0)

@@ -46,3 +46,42 @@ def test_no_join_off_gpu():
     from sqr.conv import ResidualJoin
     x = torch.zeros(1, 8, 4, 4, dtype=torch.bfloat16, requires_grad=True)
     assert ResidualJoin.make(x) is None  # CPU tensors: torch's own autograd add
+
+
+def test_untaken_deposit_raises_at_end_of_backward():
+    """A deposit that conv1's backward never takes in the same backward pass would silently drop the
+    residual branch's gradient: the join's end-of-backward callback raises instead."""
+    import pytest
+    j = _join()
+
+    class Branch(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 2
+
+        @staticmethod
+        def backward(ctx, g):
+            return j.deposit(g * 2)
+
+    x = torch.ones(3, requires_grad=True)
+    with pytest.raises(RuntimeError, match="ResidualJoin"):
+        Branch.apply(x).sum().backward()
+    assert j.pending is None
+
+    # taken inside the same pass: no error, and the consumer got it
+    got = []
+
+    class Conv1(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 3
+
+        @staticmethod
+        def backward(ctx, g):
+            add = j.take()
+            got.append(add)
+            return g * 3 + (add if add is not None else 0)
+
+    x = torch.ones(3, requires_grad=True)
+    (Branch.apply(x) + Conv1.apply(x)).sum().backward()
+    assert torch.equal(x.grad, torch.full((3,), 5.0))

@@ -42,9 +42,9 @@ def _rel_err(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("config,batch", [(2, 64), (4, 64), (5, 4)],
-                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B4"])
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("config,batch", [(2, 64), (4, 64), (5, 16)],
+                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B16"])
 def test_bench_step_gradients_vs_f64(config, batch):
     import bench
     import ref_torch

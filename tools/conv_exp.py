@@ -1,7 +1,6 @@
 """Time one conv kernel in isolation on the GPU: REPS launches captured in a HIP graph, each launch's
 own wall-clock span read back through the clock probe (sqr_probe_arm_clock), median over a few
-replays.  Used for kernel experiments (SQR_EXP ablation builds via SQR_LIB, tile configurations via
-SQR_D3_CFG / SQR_NT_CFG).
+replays.  Used for kernel experiments (an alternative build of the library via SQR_LIB).
 
     python tools/conv_exp.py --shape 64,64,64,64 --phase fwd [--dtype bf16] [--reps 20]
 Prints one JSON line: {"shape", "phase", "us": median per-launch us, "tflops", "lib"}.

@@ -2,7 +2,7 @@
 # A/B bench on ONE box (MI355X devices differ by up to ~10% on MFMA-bound kernels, so compare
 # variants only within a call): alternates the variants ROUNDS times.
 #   gpurun -- bash tools/gpu_ab.sh TAG ROUNDS "ENV_A" "ENV_B" [bench args...]
-# e.g. bash tools/gpu_ab.sh r02r 3 "SQR_BN_ADD=1" "SQR_BN_ADD=0" --config 2
+# e.g. bash tools/gpu_ab.sh r03a 3 "SQR_LIB=sq-recovery_amd/sqr/libsqr.so" "SQR_LIB=build/alt/libsqr.so" --config 2
 set -euo pipefail
 TAG=$1; ROUNDS=$2; A=$3; B=$4; shift 4
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
