@@ -267,6 +267,35 @@ def time_loss_call(crit, images, B, dev, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+# the probe kernel's forward instance in rocprofv3 kernel names (tools/traffic.py FWD_RE: the
+# statistics-producing conv3p_kernel<T, STATS=true, ACC=false, BNB=false>, mangled or demangled)
+_PROBE_RE = r"conv3p_kernel(IDF16b?Lb1E|<[^<>]*?,\s*true,|<bool _Accum, bool, E, false, false>)"
+
+
+def pmc_summary(H, dname):
+    """MFMA-busy and issue counters of the step's kernels from the committed rocprofv3 PMC summary
+    (profiles/pmc_step.json, written by tools/pmc_step.py from tools/gpu_pmc_step.sh on the default
+    config-2 step): the probe kernel's counters and the step-wide MFMA utilisation (MFMA-busy cycles of
+    every kernel over every kernel's duration x 1024 SIMDs)."""
+    import re
+    path = os.path.join(ROOT, "profiles", "pmc_step.json")
+    if not os.path.exists(path) or H != 256 or dname != "bf16":
+        return None
+    with open(path) as f:
+        rows = json.load(f)
+    out = {"source": "profiles/pmc_step.json (rocprofv3 --pmc, eager step, mean per dispatch)"}
+    probe = [r for r in rows if re.search(_PROBE_RE, r["kernel"])]
+    if probe:
+        r = probe[0]
+        out["probe"] = {k: r.get(k) for k in ("kernel", "mfma_busy", "wait_any_frac", "wait_inst_any_frac",
+                                              "active_inst_any_frac", "lds_conflict", "insts_valu", "hbm_bytes")}
+    busy = sum(r.get("mfma_busy", 0.0) * r["gpu_cycles"] * r.get("dispatches", 1) for r in rows)
+    cyc = sum(r["gpu_cycles"] * r.get("dispatches", 1) for r in rows)
+    if cyc:
+        out["step_mfma_busy"] = busy / cyc
+    return out
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -436,6 +465,10 @@ def main():
                 trf = json.load(f)
             if trf.get("kernel_key") == list(PROBE) and H == 256 and dname == "bf16":
                 roof["traffic"] = trf.get("hbm_bytes_per_launch")
+        pmc = pmc_summary(H, dname)
+        if pmc:
+            roof["mfma_busy"] = pmc.get("probe", {}).get("mfma_busy")
+            roof["pmc"] = pmc
         out["roofline"] = roof
         # secondary rooflines: the whole step's conv work against the MFMA peak, and
         # the fused loss call against the transcendental rate (per voxel ~21 exp2/log2/rcp, fwd + bwd)

@@ -28,25 +28,85 @@ __global__ void __launch_bounds__(256) reduce_kernel(const T* __restrict__ x, co
   reduce_block<T, MODE>(x, dy, mask, mean, M, C, chunk, part, blockIdx.x, red);
 }
 
-template <typename P>
-__device__ __forceinline__ bool sum_partials(const P* __restrict__ part, int nblk, int C, double* s, int* cout) {
-  *cout = blockIdx.x;
-  return sum_partials_c<P>(part, nblk, C, blockIdx.x, s);
+// Forward statistics of one block of `chunk` pixels (the internal reduction when no conv epilogue
+// produced them): two passes over the block's pixels — its mean, then the sum of squared deviations
+// from that (fp32-rounded) mean — written as the Welford row (mean_t, M2_t) of part[blk] plus its
+// pixel count (merge_stats_w).  Pass 2 re-reads the block's chunk (L2-resident).
+template <typename T>
+__global__ void __launch_bounds__(256) fwd_stats_kernel(const T* __restrict__ x, int M, int C, int chunk,
+                                                        double* __restrict__ part) {
+  extern __shared__ double red[];  // [rows][V][8] + C means
+  const int V = C >> 3, rows = 256 / V;
+  const int tid = threadIdx.x, row = tid / V, v = tid - row * V;
+  const int blk = blockIdx.x, nblk = gridDim.x;
+  const int p0 = blk * chunk, p1 = min(p0 + chunk, M);
+  double* mu_l = red + (size_t)rows * V * 8;
+  constexpr int U = 8;
+  auto pass = [&](bool second, const float* mu) {
+    double acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.0;
+    for (int pb = p0 + row; pb < p1; pb += U * rows) {
+      float xv[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) V8<T>::load(x + (size_t)min(pb + u * rows, p1 - 1) * C + v * 8, xv[u]);
+      float f[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool in = pb + u * rows < p1;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = second ? xv[u][i] - mu[i] : xv[u][i];
+          f[i] += in ? (second ? d * d : d) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += (double)f[i];
+    }
+    double* dst = red + ((size_t)row * V + v) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dst[i] = acc[i];
+    __syncthreads();
+  };
+  auto colsum = [&](int t) {  // fixed-order sum over the rows of channel t
+    const int vv = t >> 3, i = t & 7;
+    double s = 0.0;
+    for (int r = 0; r < rows; ++r) s += red[((size_t)r * V + vv) * 8 + i];
+    return s;
+  };
+  const double n = (double)(p1 - p0);
+  pass(false, nullptr);
+  for (int t = tid; t < C; t += 256) mu_l[t] = (double)(float)(colsum(t) / n);  // the row mean, fp32-rounded
+  __syncthreads();
+  float mu[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mu[i] = (float)mu_l[v * 8 + i];
+  __syncthreads();  // the first pass's sums are consumed
+  pass(true, mu);
+  for (int t = tid; t < C; t += 256) {
+    part[(size_t)blk * 2 * C + t] = mu_l[t];
+    part[(size_t)blk * 2 * C + C + t] = colsum(t);
+  }
+  if (tid == 0) part[(size_t)nblk * 2 * C + blk] = n;
 }
 
-// forward finalize: coef[0][c] = scale, coef[1][c] = shift; save_mean/save_invstd; running stats
+// forward finalize: coef[0][c] = scale, coef[1][c] = shift; save_mean/save_invstd; running stats.
+// part: Welford rows + counts (merge_stats_w), f32 from a conv epilogue / the stem, f64 from
+// fwd_stats_kernel
 template <typename P>
 __global__ void fwd_finalize_kernel(const P* __restrict__ part, int nblk, int M, int C,
                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                     float* __restrict__ rmean, float* __restrict__ rvar, float momentum, float eps,
                                     float* __restrict__ save_mean, float* __restrict__ save_invstd,
                                     float* __restrict__ coef) {
-  double acc[2];
-  int c;
-  if (!sum_partials(part, nblk, C, acc, &c)) return;
-  const double s = acc[0], ss = acc[1];
-  const double mean = s / M;
-  double var = ss / M - mean * mean;
+  const int c = fin_wave_index();
+  if (c >= C) return;
+  double mean, m2;
+  merge_stats_w<P>(part, nblk, C, c, (double)M, &mean, &m2);
+  if (threadIdx.x & 63) return;
+  double var = m2 / M;
   var = var < 0.0 ? 0.0 : var;
   const double invstd = 1.0 / sqrt(var + (double)eps);
   const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
@@ -117,7 +177,8 @@ __global__ void bwd_finalize_kernel(const P* __restrict__ part, int nblk, int M,
                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, float* __restrict__ dgamma,
                                     float* __restrict__ dbeta, float* __restrict__ coef) {
-  bn_bwd_finalize_c<P>(part, nblk, M, C, blockIdx.x, gamma, mean, invstd, dgamma, dbeta, coef);
+  const int c = fin_wave_index();
+  if (c < C) bn_bwd_finalize_w<P>(part, nblk, M, C, c, gamma, mean, invstd, dgamma, dbeta, coef);
 }
 
 // dx = k1*g + k3*x + k2 with g = dy*[relu bit]; optionally dres = g
@@ -213,9 +274,8 @@ struct FinJob {
   float *dgamma, *dbeta;
 };
 
-__device__ __forceinline__ void fwd_finalize_one(const FinJob& j, int c, int M, int C, double s, double ss) {
-  const double mean = s / M;
-  double var = ss / M - mean * mean;
+__device__ __forceinline__ void fwd_finalize_one(const FinJob& j, int c, int M, int C, double mean, double m2) {
+  double var = m2 / M;
   var = var < 0.0 ? 0.0 : var;
   const double invstd = 1.0 / sqrt(var + (double)j.eps);
   const float g = j.gamma ? j.gamma[c] : 1.f, bt = j.beta ? j.beta[c] : 0.f;
@@ -232,12 +292,15 @@ __device__ __forceinline__ void fwd_finalize_one(const FinJob& j, int c, int M, 
 
 // grid 2C: blocks [0, C) finalize BN a, [C, 2C) BN b (same arithmetic as fwd_finalize_kernel)
 __global__ void fwd_finalize2_kernel(FinJob a, FinJob b, int M, int C) {
-  const bool second = (int)blockIdx.x >= C;
+  const int w = fin_wave_index();
+  if (w >= 2 * C) return;
+  const bool second = w >= C;
   const FinJob& j = second ? b : a;
-  const int c = second ? blockIdx.x - C : blockIdx.x;
-  double acc[2];
-  if (!sum_partials_c<float>(j.part, j.nblk, C, c, acc)) return;
-  fwd_finalize_one(j, c, M, C, acc[0], acc[1]);
+  const int c = second ? w - C : w;
+  double mean, m2;
+  merge_stats_w<float>(j.part, j.nblk, C, c, (double)M, &mean, &m2);
+  if (threadIdx.x & 63) return;
+  fwd_finalize_one(j, c, M, C, mean, m2);
 }
 
 // y = act(xa*sa + ta + xb*sb + tb)
@@ -284,13 +347,17 @@ __global__ void __launch_bounds__(256) reduce2_kernel(const T* __restrict__ xa, 
 
 // grid 2C: BN a from (sum g, sum g*(xa-mean_a)), BN b from (sum g, sum g*(xb-mean_b))
 __global__ void bwd_finalize2_kernel(const double* __restrict__ part, int nblk, int M, int C, FinJob a, FinJob b) {
-  const bool second = (int)blockIdx.x >= C;
+  const int w = fin_wave_index();
+  if (w >= 2 * C) return;
+  const bool second = w >= C;
   const FinJob& j = second ? b : a;
-  const int c = second ? blockIdx.x - C : blockIdx.x;
+  const int c = second ? w - C : w;
   double acc[2];
-  const bool mine = second ? sum_partials_c<double, 3, 2>(part, nblk, C, c, acc)
-                           : sum_partials_c<double, 3, 1>(part, nblk, C, c, acc);
-  if (!mine) return;
+  if (second)
+    sum_partials_w<double, 3, 2>(part, nblk, C, c, acc);
+  else
+    sum_partials_w<double, 3, 1>(part, nblk, C, c, acc);
+  if (threadIdx.x & 63) return;
   const double sg = acc[0], sgx = acc[1];
   const double is = j.save_invstd[c], mu = j.save_mean[c];
   const double dgam = sgx * is;
@@ -554,7 +621,7 @@ using namespace sqr::bn;
 int sqr::bn_finalize_partials(const float* part, int rows, long long M, int C, const float* gamma, const float* beta,
                               float* rmean, float* rvar, float momentum, float eps, float* save_mean,
                               float* save_invstd, float* coef, hipStream_t st) {
-  hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, part, rows, (int)M, C, gamma, beta, rmean,
+  hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(fin_blocks(C)), dim3(256), 0, st, part, rows, (int)M, C, gamma, beta, rmean,
                      rvar, momentum, eps, save_mean, save_invstd, coef);
   SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel(partials)");
   return 0;
@@ -589,6 +656,8 @@ RedPlan red_plan(int M, int C) {
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+size_t fwd_stats_lds(const RedPlan& p, int C) { return ((size_t)p.rows * (C / 8) * 8 + C) * sizeof(double); }
+
 int check_mc(long long M, int C, int dtype) {
   SQR_CHECK_ARG(M >= 1 && M < (1ll << 31), "bn: bad pixel count %lld", M);
   SQR_CHECK_ARG(C >= 8 && C <= 2048 && C % 8 == 0 && (256 % (C / 8) == 0 || C / 8 > 256),
@@ -606,7 +675,7 @@ unsigned ew_grid(long long nvec) { return (unsigned)((nvec + 255) / 256); }
 extern "C" size_t sqr_bn_workspace_bytes(long long M, int C) {
   if (M < 1 || C < 8) return 0;
   const RedPlan p = red_plan((int)M, C);
-  return a256((size_t)p.nblk * 2 * C * sizeof(double)) + a256((size_t)3 * C * sizeof(float));
+  return a256((size_t)p.nblk * (2 * C + 1) * sizeof(double)) + a256((size_t)3 * C * sizeof(float));
 }
 
 
@@ -618,16 +687,16 @@ static int bn_fwd_impl(const void* x, int M, int C, const float* gamma, const fl
                        int ext_rows = 0) {
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
-  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * (2 * C + 1) * sizeof(double)));
   if (training && ext) {  // statistics partials produced by the conv epilogue
-    hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, ext, ext_rows, M, C, gamma, beta,
+    hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(fin_blocks(C)), dim3(256), 0, st, ext, ext_rows, M, C, gamma, beta,
                        rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel(ext)");
   } else if (training) {
-    hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
-                       (const uint8_t*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
+    hipLaunchKernelGGL((fwd_stats_kernel<T>), dim3(p.nblk), dim3(256), fwd_stats_lds(p, C), st, (const T*)x, M, C,
+                       p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("bn reduce_kernel");
-    hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+    hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(fin_blocks(C)), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("bn fwd_finalize_kernel");
   } else {
@@ -672,11 +741,11 @@ static int bn_bwd_impl(const void* dy, const uint8_t* mask, const void* x, int M
                        void* ws, hipStream_t st) {
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
-  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * (2 * C + 1) * sizeof(double)));
   hipLaunchKernelGGL((reduce_kernel<T, 1>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)dy,
                      mask, mean, M, C, p.chunk, part);
   SQR_HIP_LAUNCH_CHECK("bn bwd reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(fin_blocks(C)), dim3(256), 0, st, part, p.nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel");
   const int nvec = M * (C / 8);
@@ -720,16 +789,16 @@ static int stem_fwd_impl(const void* x, int N, int H, int W, int C, const float*
   const int M = N * H * W;
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
-  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  float* coef = (float*)((char*)ws + a256((size_t)p.nblk * (2 * C + 1) * sizeof(double)));
   if (training && ext) {
-    hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, ext, ext_rows, M, C, gamma, beta,
+    hipLaunchKernelGGL(fwd_finalize_kernel<float>, dim3(fin_blocks(C)), dim3(256), 0, st, ext, ext_rows, M, C, gamma, beta,
                        rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel(ext)");
   } else if (training) {
-    hipLaunchKernelGGL((reduce_kernel<T, 0>), dim3(p.nblk), dim3(256), p.lds, st, (const T*)x, (const T*)nullptr,
-                       (const uint8_t*)nullptr, (const float*)nullptr, M, C, p.chunk, part);
+    hipLaunchKernelGGL((fwd_stats_kernel<T>), dim3(p.nblk), dim3(256), fwd_stats_lds(p, C), st, (const T*)x, M, C,
+                       p.chunk, part);
     SQR_HIP_LAUNCH_CHECK("stem reduce_kernel");
-    hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, p.nblk, M, C, gamma,
+    hipLaunchKernelGGL(fwd_finalize_kernel<double>, dim3(fin_blocks(C)), dim3(256), 0, st, part, p.nblk, M, C, gamma,
                        beta, rmean, rvar, momentum, eps, save_mean, save_invstd, coef);
     SQR_HIP_LAUNCH_CHECK("stem fwd_finalize_kernel");
   } else {
@@ -776,7 +845,7 @@ static int stem_bwd_impl(const void* dpool, const void* ypool, const uint8_t* ar
   const int M = N * H * W;
   const RedPlan p = red_plan(M, C);
   double* part = (double*)ws;
-  float* bcoef = (float*)((char*)ws + a256((size_t)p.nblk * 2 * C * sizeof(double)));
+  float* bcoef = (float*)((char*)ws + a256((size_t)p.nblk * (2 * C + 1) * sizeof(double)));
   const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   const int nqv = N * Ho * Wo * (C / 8);
   int chunk = (nqv + p.nblk - 1) / p.nblk;
@@ -786,7 +855,7 @@ static int stem_bwd_impl(const void* dpool, const void* ypool, const uint8_t* ar
                      (const T*)dpool, (const T*)ypool, arg, (const T*)x, mean, N, H, W, C, Ho, Wo, chunk,
                      make_fastdiv(Wo), make_fastdiv(Ho), part);
   SQR_HIP_LAUNCH_CHECK("stem_bwd_reduce_kernel");
-  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, nblk, M, C, gamma, mean,
+  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(fin_blocks(C)), dim3(256), 0, st, part, nblk, M, C, gamma, mean,
                      invstd, dgamma, dbeta, bcoef);
   SQR_HIP_LAUNCH_CHECK("stem bwd_finalize_kernel");
   hipLaunchKernelGGL((stem_bwd_apply_kernel<T>), dim3(ew_grid(nqv)), dim3(256), 0, st, (const T*)dpool,
@@ -907,7 +976,7 @@ static int bn_add_fwd_impl(const sqr_bn_operand* a, const sqr_bn_operand* b, int
   float* ca = (float*)((char*)ws + a256((size_t)p.nblk * 3 * C * sizeof(double)));
   float* cb = ca + 3 * C;
   if (training) {
-    hipLaunchKernelGGL(fwd_finalize2_kernel, dim3(2 * C), dim3(256), 0, st, fin_job(a, ca), fin_job(b, cb), M, C);
+    hipLaunchKernelGGL(fwd_finalize2_kernel, dim3(fin_blocks(2 * C)), dim3(256), 0, st, fin_job(a, ca), fin_job(b, cb), M, C);
     SQR_HIP_LAUNCH_CHECK("bn fwd_finalize2_kernel");
   } else {
     int rc = bn_infer_coef(C, a->gamma, a->beta, a->running_mean, a->running_var, a->eps, ca, st);
@@ -963,7 +1032,7 @@ static int bn_add_bwd_impl(const sqr_bn_operand* a, const sqr_bn_operand* b, con
   ja.dbeta = dba;
   jb.dgamma = dgb;
   jb.dbeta = dbb;
-  hipLaunchKernelGGL(bwd_finalize2_kernel, dim3(2 * C), dim3(256), 0, st, part, p.nblk, M, C, ja, jb);
+  hipLaunchKernelGGL(bwd_finalize2_kernel, dim3(fin_blocks(2 * C)), dim3(256), 0, st, part, p.nblk, M, C, ja, jb);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize2_kernel");
   const int nvec = M * (C / 8);
   hipLaunchKernelGGL((bwd_apply2_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dy, mask,
@@ -1023,7 +1092,7 @@ static int bn_bwd_stats_impl(const void* g, const void* x, int M, int C, const f
                              const float* gamma, const float* mean, const float* invstd, void* dx, float* dgamma,
                              float* dbeta, void* ws, hipStream_t st) {
   float* coef = (float*)ws;
-  hipLaunchKernelGGL(bwd_finalize_kernel<float>, dim3(C), dim3(256), 0, st, stats, rows, M, C, gamma, mean, invstd,
+  hipLaunchKernelGGL(bwd_finalize_kernel<float>, dim3(fin_blocks(C)), dim3(256), 0, st, stats, rows, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel(stats)");
   const int nvec = M * (C / 8);
@@ -1094,7 +1163,7 @@ static int bn_bwd_part_impl(const void* dy, const uint8_t* mask, const void* x, 
                             int rows, const float* gamma, const float* mean, const float* invstd, void* dx, void* dres,
                             float* dgamma, float* dbeta, void* ws, hipStream_t st) {
   float* coef = (float*)ws;
-  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(C), dim3(256), 0, st, part, rows, M, C, gamma, mean, invstd,
+  hipLaunchKernelGGL(bwd_finalize_kernel<double>, dim3(fin_blocks(C)), dim3(256), 0, st, part, rows, M, C, gamma, mean, invstd,
                      dgamma, dbeta, coef);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize_kernel(part)");
   const int nvec = M * (C / 8);
@@ -1137,7 +1206,7 @@ static int bn_add_bwd_part_impl(const sqr_bn_operand* a, const sqr_bn_operand* b
   ja.dbeta = dba;
   jb.dgamma = dgb;
   jb.dbeta = dbb;
-  hipLaunchKernelGGL(bwd_finalize2_kernel, dim3(2 * C), dim3(256), 0, st, part, rows, M, C, ja, jb);
+  hipLaunchKernelGGL(bwd_finalize2_kernel, dim3(fin_blocks(2 * C)), dim3(256), 0, st, part, rows, M, C, ja, jb);
   SQR_HIP_LAUNCH_CHECK("bn bwd_finalize2_kernel(part)");
   const int nvec = M * (C / 8);
   hipLaunchKernelGGL((bwd_apply2_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const T*)dy, mask,

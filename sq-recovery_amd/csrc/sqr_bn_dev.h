@@ -221,42 +221,59 @@ __device__ __forceinline__ void reduce2_block(const T* __restrict__ xa, const T*
   }
 }
 
-// one block per channel: thread t sums partials t, t+256, ... (independent loads in flight), then a
-// fixed xor-tree wave reduction and a fixed-order sum of the 4 waves (deterministic).  Returns
-// true on thread 0 only.
-// (partials [k][NS][C]: statistic 0 and statistic SB of channel c)
+// Finalize helpers: ONE WAVE per channel (a finalize launch is latency-bound: no LDS round trip or
+// workgroup barrier, four channels per 256-thread workgroup).  Lane l sums rows l, l+64, ...
+// (independent loads in flight), then a fixed xor butterfly: every lane ends with the same totals
+// (deterministic).  (partials [k][NS][C]: statistic 0 and statistic SB of channel c)
 template <typename P, int NS = 2, int SB = 1>
-__device__ __forceinline__ bool sum_partials_c(const P* __restrict__ part, int nblk, int C, int c, double* s) {
-  __shared__ double red[2][4];
-  const int t = threadIdx.x;
+__device__ __forceinline__ void sum_partials_w(const P* __restrict__ part, int nblk, int C, int c, double* s) {
+  const int l = threadIdx.x & 63;
   double a = 0.0, b = 0.0;
 #pragma unroll 4
-  for (int k = t; k < nblk; k += 256) {
+  for (int k = l; k < nblk; k += 64) {
     a += (double)part[(size_t)k * NS * C + c];
     b += (double)part[(size_t)k * NS * C + SB * C + c];
   }
-  a = wave_sum_d(a);
-  b = wave_sum_d(b);
-  if ((t & 63) == 0) {
-    red[0][t >> 6] = a;
-    red[1][t >> 6] = b;
-  }
-  __syncthreads();
-  if (t != 0) return false;
-  s[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-  s[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-  return true;
+  s[0] = wave_sum_d(a);
+  s[1] = wave_sum_d(b);
 }
-// BatchNorm backward finalize of channel c from (sum g, sum g*(x - mean)) partials [nblk][2][C]:
-// dgamma, dbeta and the dx = k1*g + k3*x + k2 coefficients coef[0..2][C].  Every thread of the
-// workgroup must call it (it reduces through LDS); thread 0 writes.
+
+// Forward batch statistics of channel c from Welford-style partial rows (every producer: conv
+// epilogues, the fused stem, fwd_stats_kernel): part[nblk][2][C] = (mean_t, M2_t) of row t's pixels
+// (M2_t = sum over them of (x - mean_t)^2, centred inside the row), followed by cnt[nblk] = the
+// rows' pixel counts.  Merged in float64 with Chan's formula, rows in a fixed order:
+//   mean = sum_t n_t mean_t / M,  M2 = sum_t (M2_t + n_t (mean_t - mean)^2)
+// — no E[x^2] - mean^2 cancellation, so a channel with |mean| >> std keeps its variance.  One wave;
+// every lane gets the results.
 template <typename P>
-__device__ __forceinline__ void bn_bwd_finalize_c(const P* __restrict__ part, int nblk, int M, int C, int c,
+__device__ __forceinline__ void merge_stats_w(const P* __restrict__ part, int nblk, int C, int c, double M,
+                                              double* mean_out, double* m2_out) {
+  const int l = threadIdx.x & 63;
+  const P* __restrict__ cnt = part + (size_t)nblk * 2 * C;
+  double a = 0.0;
+#pragma unroll 4
+  for (int k = l; k < nblk; k += 64) a += (double)cnt[k] * (double)part[(size_t)k * 2 * C + c];
+  const double mu = wave_sum_d(a) / M;
+  double b = 0.0;
+#pragma unroll 4
+  for (int k = l; k < nblk; k += 64) {
+    const double d = (double)part[(size_t)k * 2 * C + c] - mu;
+    b += (double)part[(size_t)k * 2 * C + C + c] + (double)cnt[k] * d * d;
+  }
+  *mean_out = mu;
+  *m2_out = wave_sum_d(b);
+}
+
+// BatchNorm backward finalize of channel c from (sum g, sum g*(x - mean)) partials [nblk][2][C]:
+// dgamma, dbeta and the dx = k1*g + k3*x + k2 coefficients coef[0..2][C].  One wave; lane 0 writes.
+template <typename P>
+__device__ __forceinline__ void bn_bwd_finalize_w(const P* __restrict__ part, int nblk, int M, int C, int c,
                                                   const float* __restrict__ gamma, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                   float* __restrict__ dbeta, float* __restrict__ coef) {
   double acc[2];
-  if (!sum_partials_c<P>(part, nblk, C, c, acc)) return;
+  sum_partials_w<P>(part, nblk, C, c, acc);
+  if ((threadIdx.x & 63) != 0) return;
   const double sg = acc[0], sgx = acc[1];
   const double is = invstd[c], mu = mean[c];
   const double dgam = sgx * is;  // sum g * xhat
@@ -268,6 +285,10 @@ __device__ __forceinline__ void bn_bwd_finalize_c(const P* __restrict__ part, in
   coef[2 * C + c] = (float)k3;
   coef[C + c] = (float)(-a * sg / M - k3 * mu);
 }
+
+// the channel (or job-channel) index of this wave in a finalize launch of 4 waves per workgroup
+__device__ __forceinline__ int fin_wave_index() { return (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6); }
+__host__ __device__ constexpr int fin_blocks(int channels) { return (channels + 3) / 4; }
 
 // a BatchNorm backward finalize riding along another launch (its extra workgroups)
 struct BnFinDev {

@@ -88,4 +88,41 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
   return v;
 }
 
+// ---------------------------------------------------------------- BatchNorm statistics (Welford rows)
+// Forward statistics partials are rows (mean_t, M2_t) of disjoint pixel sets plus their counts
+// (sqr_bn_dev.h merge_stats_w).  A producer builds a row from lane entries:
+//   lane:   the shifted sums of its n values v_i of a channel about its first value K
+//           (S = sum (v_i - K), Q = sum (v_i - K)^2; no cancellation while the values are within a
+//           few std of each other) -> lane mean K + S/n and M2 = Q - S^2/n
+//   row:    R lanes of equal count n merged in a fixed order, float64 accumulation:
+//           mean = sum m_l / R,  M2 = sum (M2_l + n (m_l - mean)^2)   (M2 about the stored fp32 mean)
+struct LaneStat {
+  float k, s, q;
+};
+__device__ __forceinline__ void lane_stat_add(LaneStat& a, float v, bool first) {
+  if (first) a.k = v;
+  const float d = v - a.k;
+  a.s += d;
+  a.q = fmaf(d, d, a.q);
+}
+__device__ __forceinline__ void lane_stat_final(const LaneStat& a, float n, float* mean, float* m2) {
+  const float sn = a.s / n;
+  *mean = a.k + sn;
+  *m2 = fmaxf(a.q - a.s * sn, 0.f);
+}
+// row (mean, M2) of R lane entries at src_m[r * stride], src_q[r * stride] with n values each
+__device__ __forceinline__ void lane_rows_merge(const float* src_m, const float* src_q, int R, int stride, float n,
+                                                float* mean, float* m2) {
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += (double)src_m[r * stride];
+  const float mu = (float)(s / R);
+  double q = 0.0;
+  for (int r = 0; r < R; ++r) {
+    const double d = (double)(src_m[r * stride] - mu);
+    q += (double)src_q[r * stride] + (double)n * d * d;
+  }
+  *mean = mu;
+  *m2 = (float)q;
+}
+
 }  // namespace sqr

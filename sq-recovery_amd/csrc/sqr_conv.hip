@@ -54,7 +54,7 @@ struct NTArgs {
   void* out;       // [M][Nout] (os == 1) or the strided pixel subset of an [N][oH][oW][Nout] tensor
   int os, oph, opw, oH, oW;  // out pixel of row (n,i,j) = (n, i*os+oph, j*os+opw)
   int ntm, ntn;    // tile counts
-  float* stats;    // nullable: per-M-tile BatchNorm partials [ntm][2][Nout] (sum, sum of squares)
+  float* stats;    // nullable: per-M-tile BatchNorm Welford rows [ntm][2][Nout] (mean, M2) + [ntm] counts
 };
 
 // up to 4 independent NT GEMMs in one launch (the stride-parity classes of a strided dgrad):
@@ -287,55 +287,75 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
     }
   }
   if (a.stats) {
-    // fused BatchNorm statistics of the STORED (dtype-rounded) output: per channel sum and sum of
-    // squares over this M-tile -> stats[tile_m][0/1][n]; the BN layer finalizes from these
-    // partials instead of re-reading the whole activation.
-    float* red = (float*)smem;  // [WAVES_M][BN][2]; the k loop ended with a barrier
+    // fused BatchNorm statistics of the STORED (dtype-rounded) output: this M-tile's Welford row
+    // (mean, M2) per channel -> stats[tile_m][0/1][n] and its pixel count after the ntm rows (the BN
+    // layer finalizes from these partials instead of re-reading the whole activation).  Lanes: shifted
+    // sums of their valid pixels (sqr_common.h LaneStat), merged over the 16 pixel lanes by an xor
+    // tree and over the WAVES_M wave rows in order, both with Chan's formula (counts may differ in a
+    // partial last tile).
+    float* red = (float*)smem;  // [WAVES_M][BN][3]; the k loop ended with a barrier
+    auto chan = [](float& n, float& m, float& q, float nb, float mb, float qb) {
+      const float nn = n + nb;
+      if (nb == 0.f) return;
+      if (n == 0.f) {
+        n = nb, m = mb, q = qb;
+        return;
+      }
+      const float d = mb - m;
+      m = m + d * (nb / nn);
+      q = q + qb + d * d * (n * nb / nn);
+      n = nn;
+    };
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wm * WM + 16 * i + fr;
-        if (m < g.M) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float v = (float)(T)acc[j][i][e];
-            s1[e] += v;
-            s2[e] = fmaf(v, v, s2[e]);
-          }
-        }
-      }
+      float cn[4], cm[4], cq[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        LaneStat ls = {0.f, 0.f, 0.f};
+        float n = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wm * WM + 16 * i + fr;
+          if (m < g.M) {
+            lane_stat_add(ls, (float)(T)acc[j][i][e], n == 0.f);
+            n += 1.f;
+          }
+        }
+        cn[e] = n;
+        if (n > 0.f) {
+          lane_stat_final(ls, n, &cm[e], &cq[e]);
+        } else {
+          cm[e] = cq[e] = 0.f;
+        }
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
-          s1[e] += __shfl_xor(s1[e], off, 64);
-          s2[e] += __shfl_xor(s2[e], off, 64);
+          const float nb = __shfl_xor(cn[e], off, 64), mb = __shfl_xor(cm[e], off, 64),
+                      qb = __shfl_xor(cq[e], off, 64);
+          chan(cn[e], cm[e], cq[e], nb, mb, qb);
         }
       }
       if (fr == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int col = wn * WN + 16 * j + 4 * fq + e;
-          red[(wm * BN + col) * 2] = s1[e];
-          red[(wm * BN + col) * 2 + 1] = s2[e];
+          red[(wm * BN + col) * 3] = cn[e];
+          red[(wm * BN + col) * 3 + 1] = cm[e];
+          red[(wm * BN + col) * 3 + 2] = cq[e];
         }
       }
     }
     __syncthreads();
     for (int t = tid; t < BN; t += NT) {
-      float a1 = 0.f, a2 = 0.f;
+      float n = 0.f, m = 0.f, q = 0.f;
 #pragma unroll
-      for (int w = 0; w < WAVES_M; ++w) {
-        a1 += red[(w * BN + t) * 2];
-        a2 += red[(w * BN + t) * 2 + 1];
+      for (int w = 0; w < WAVES_M; ++w)
+        chan(n, m, q, red[(w * BN + t) * 3], red[(w * BN + t) * 3 + 1], red[(w * BN + t) * 3 + 2]);
+      const int nc = n0 + t;
+      if (nc < a.Nout) {
+        a.stats[((size_t)tile_m * 2) * a.Nout + nc] = m;
+        a.stats[((size_t)tile_m * 2 + 1) * a.Nout + nc] = q;
       }
-      const int n = n0 + t;
-      if (n < a.Nout) {
-        a.stats[((size_t)tile_m * 2) * a.Nout + n] = a1;
-        a.stats[((size_t)tile_m * 2 + 1) * a.Nout + n] = a2;
-      }
+      if (t == 0 && n0 == 0) a.stats[(size_t)a.ntm * 2 * a.Nout + tile_m] = n;
     }
   }
   clock_end(mc.tp);
@@ -567,7 +587,7 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
 // flight), then the ZL partial sums are added in a fixed order through LDS -> deterministic.
 // The permuted writes to torch's KCRS layout are 4-B scatters (the output is small).
 // Workgroups past the reduction's own (blockIdx.x >= nred) do BatchNorm work instead, riding along
-// this launch instead of taking launches of their own: fin.C workgroups finalize the backward of
+// this launch instead of taking launches of their own: fin.C waves (4 per workgroup) finalize the backward of
 // the BatchNorm whose sums this conv's backward-data epilogue produced (one channel each), then
 // rj.nblk workgroups reduce the backward sums of the BatchNorm whose output gradient this conv's
 // backward-data just wrote (the previous block's bn2 / bn2 + downsample-bn).
@@ -578,11 +598,15 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   extern __shared__ double ride_lds[];
   if ((int)blockIdx.x >= nred) {
     const int b = blockIdx.x - nred;
-    if (b < fin.C)
-      bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, b, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
-                                   fin.dbeta, fin.coef);
-    else
-      bn::bn_reduce_ride(rj, b - fin.C, ride_lds);
+    const int nfin = bn::fin_blocks(fin.C);  // one wave per channel
+    if (b < nfin) {
+      const int c = b * 4 + (int)(threadIdx.x >> 6);
+      if (c < fin.C)
+        bn::bn_bwd_finalize_w<float>(fin.part, fin.nblk, fin.M, fin.C, c, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
+                                     fin.dbeta, fin.coef);
+    } else {
+      bn::bn_reduce_ride(rj, b - nfin, ride_lds);
+    }
     return;
   }
   __shared__ f32x4 part[256];
@@ -640,11 +664,15 @@ __global__ void __launch_bounds__(256) wgrad_reduce_tc_kernel(const float* __res
   extern __shared__ double ride_lds[];
   if ((int)blockIdx.x >= nred) {  // riding BatchNorm work (see wgrad_reduce_kernel)
     const int b = blockIdx.x - nred;
-    if (b < fin.C)
-      bn::bn_bwd_finalize_c<float>(fin.part, fin.nblk, fin.M, fin.C, b, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
-                                   fin.dbeta, fin.coef);
-    else
-      bn::bn_reduce_ride(rj, b - fin.C, ride_lds);
+    const int nfin = bn::fin_blocks(fin.C);  // one wave per channel
+    if (b < nfin) {
+      const int c = b * 4 + (int)(threadIdx.x >> 6);
+      if (c < fin.C)
+        bn::bn_bwd_finalize_w<float>(fin.part, fin.nblk, fin.M, fin.C, c, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
+                                     fin.dbeta, fin.coef);
+    } else {
+      bn::bn_reduce_ride(rj, b - nfin, ride_lds);
+    }
     return;
   }
   __shared__ f32x4 part[256];
@@ -1036,7 +1064,7 @@ int launch_wgrad_reduce(const float* slab, int splits, int K, int Ng, int C, int
   bn::BnRedDev r = {};
   if (fin) f = *fin;
   if (red) r = *red;
-  const int nride = (fin ? fin->C : 0) + (red ? red->nblk : 0);
+  const int nride = (fin ? bn::fin_blocks(fin->C) : 0) + (red ? red->nblk : 0);
   const size_t lds = red ? red_lds : 0;
   if (!im2col && Ci == C && C % 64 == 0 && RS <= 16 && splits <= 16) {
     const int zlg = reduce_zl_log2(splits, 256 / (RS * 16));
@@ -1177,7 +1205,7 @@ extern "C" int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const 
 extern "C" size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d) {
   Shape sh;
   if (check_desc(d, &sh)) return 0;
-  return (size_t)((sh.M + 63) / 64) * 2 * d->K;
+  return (size_t)((sh.M + 63) / 64) * (2 * d->K + 1);  // rows of (mean, M2) + a count per row
 }
 
 extern "C" int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,

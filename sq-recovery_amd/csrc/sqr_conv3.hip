@@ -62,27 +62,10 @@ __device__ __forceinline__ void dma_pieces(__amdgpu_buffer_rsrc_t srd, char* dst
                                              16, voff[i], soff, 0, 0);
 }
 
-// BatchNorm partials of a BM x BN output tile held as acc[j][i] (lane: pixel 16i+fr of its wave
-// rows, channels 16j+4fq..+3 of its wave columns), from the bf16 values actually stored.
-// Per-lane sums over i (stats_accum), then an LDS transpose (stats_reduce): red[wave-row
-// group][fr][col] -> one thread per column adds its 16*WAVES_M partials in a fixed order
-// (deterministic, no cross-lane shuffles).
-template <typename T, int TM, int TN>
-__device__ __forceinline__ void stats_accum(const uint32_t (*pk)[TM][2], float (*s1)[4], float (*s2)[4]) {
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float lo = lo2f<T>(pk[j][i][h]), hi = hi2f<T>(pk[j][i][h]);
-        s1[j][2 * h] += lo;
-        s2[j][2 * h] = fmaf(lo, lo, s2[j][2 * h]);
-        s1[j][2 * h + 1] += hi;
-        s2[j][2 * h + 1] = fmaf(hi, hi, s2[j][2 * h + 1]);
-      }
-}
-
+// Backward sums of a BM x BN output tile (BNB: sum g, sum g*(x - mean)) held as per-lane partials
+// s1, s2 (lane: pixel 16i+fr of its wave rows, channels 16j+4fq..+3 of its wave columns): an LDS
+// transpose red[wave-row group][fr][col], then one thread per column adds its 16*WAVES_M partials
+// in a fixed order (deterministic, no cross-lane shuffles).
 template <int BN, int WAVES_M, int WAVES_N, int TN, int NT>
 __device__ __forceinline__ void stats_reduce(const float (*s1)[4], const float (*s2)[4], float* red, int wm, int wn,
                                              int fr, int fq, int tid, float* stats_row0, float* stats_row1) {
@@ -106,18 +89,41 @@ __device__ __forceinline__ void stats_reduce(const float (*s1)[4], const float (
   }
 }
 
-// BatchNorm partials of a BM x BN output tile held as acc[j][i] (lane: pixel 16i+fr of its wave
-// rows, channels 16j+4fq..+3 of its wave columns), from the 16-bit values actually stored.
+// Forward BatchNorm statistics of a BM x BN output tile held as acc[j][i], from the 16-bit values
+// actually stored: the tile's Welford row (mean, M2) per channel (sqr_common.h LaneStat): each lane
+// has TM values of each of its channels (pixels 16i+fr), shifted about its first one; the
+// WAVES_M*16 lane entries of a column go through the same LDS transpose and are merged by one
+// thread per column.  Row count BM (written once per tile row by the tile_n = 0 workgroup).
 template <typename T, int BN, int WAVES_M, int WAVES_N, int TM, int TN, int NT>
 __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* red, int wm, int wn, int fr, int fq,
-                                           int tid, float* stats_row0, float* stats_row1) {
-  float s1[TN][4], s2[TN][4];
+                                           int tid, float* stats_row0, float* stats_row1, float* count, float bm) {
+  constexpr int WN = BN / WAVES_N, R = WAVES_M * 16;
+  float* r1 = red + (wm * 16 + fr) * BN + wn * WN + 4 * fq;
+  float* r2 = r1 + R * BN;
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+  for (int j = 0; j < TN; ++j) {
+    float m[4], q[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s1[j][e] = s2[j][e] = 0.f;
-  stats_accum<T, TM, TN>(pk, s1, s2);
-  stats_reduce<BN, WAVES_M, WAVES_N, TN, NT>(s1, s2, red, wm, wn, fr, fq, tid, stats_row0, stats_row1);
+    for (int e = 0; e < 4; ++e) {
+      LaneStat a = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const uint32_t p = pk[j][i][e >> 1];
+        lane_stat_add(a, (e & 1) ? hi2f<T>(p) : lo2f<T>(p), i == 0);
+      }
+      lane_stat_final(a, (float)TM, &m[e], &q[e]);
+    }
+    *(f32x4*)(r1 + 16 * j) = f32x4{m[0], m[1], m[2], m[3]};
+    *(f32x4*)(r2 + 16 * j) = f32x4{q[0], q[1], q[2], q[3]};
+  }
+  __syncthreads();
+  for (int col = tid; col < BN; col += NT) {
+    float mean, m2;
+    lane_rows_merge(red + col, red + R * BN + col, R, BN, (float)TM, &mean, &m2);
+    stats_row0[col] = mean;
+    stats_row1[col] = m2;
+  }
+  if (count && tid == 0) *count = bm;
 }
 
 // IMGS > 1: a tile is IMGS whole images (TH x TW = H x W) with one halo window each, stacked in LDS
@@ -396,7 +402,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   if (!BNB && a.stats)
     tile_stats<T, BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
                                                  a.stats + ((size_t)tile_m * 2) * a.Nout + n0,
-                                                 a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
+                                                 a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0,
+                                                 tile_n == 0 ? a.stats + (size_t)a.ntm * 2 * a.Nout + tile_m : nullptr,
+                                                 (float)BM);
   clock_end(a.tp);
 }
 
@@ -520,10 +528,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
 
   // 32x32x16 operand lanes: row r32 = lane & 31 (pixel / output channel), k half h = lane >> 5
   const int flip = a.flip;
-  // BatchNorm partials (this lane: pixel column, 16 channels wn*32 + 8g + 4h + e) over all tiles
-  float st1[16], st2[16];
+  // BatchNorm statistics (this lane: pixel column, 16 channels wn*32 + 8g + 4h + e) over all tiles:
+  // shifted sums about the lane's first value of each channel (sqr_common.h LaneStat)
+  LaneStat ls[STATS ? 16 : 1];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) st1[e] = st2[e] = 0.f;
+  for (int e = 0; e < (STATS ? 16 : 1); ++e) ls[e] = LaneStat{0.f, 0.f, 0.f};
 
   u32x4 av[NST];  // ACC: the addend pieces of the tile stored next; BNB: the BatchNorm input x there
   uint32_t bm[BNB ? NST : 1];  // BNB: the mask byte of each piece (8 channels)
@@ -671,11 +680,8 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         pk[i][g][1] = pack2<T>(acc[i][4 * g + 2], acc[i][4 * g + 3]);
 #pragma unroll
         for (int q = 0; q < 2 * STATS; ++q) {
-          const float v0 = lo2f<T>(pk[i][g][q]), v1 = hi2f<T>(pk[i][g][q]);
-          st1[4 * g + 2 * q] += v0;
-          st2[4 * g + 2 * q] = fmaf(v0, v0, st2[4 * g + 2 * q]);
-          st1[4 * g + 2 * q + 1] += v1;
-          st2[4 * g + 2 * q + 1] = fmaf(v1, v1, st2[4 * g + 2 * q + 1]);
+          lane_stat_add(ls[4 * g + 2 * q], lo2f<T>(pk[i][g][q]), k == 0 && i == 0);
+          lane_stat_add(ls[4 * g + 2 * q + 1], hi2f<T>(pk[i][g][q]), k == 0 && i == 0);
         }
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -725,20 +731,27 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = col_sum(red + sl * 16 + 8 * q + e, NT / 8, 8 * 16);
     }
   }
-  if (STATS) {  // red[2][64 pixel lanes][64 channels] -> fixed-order column sums
+  if constexpr (STATS) {  // red[2][64 pixel lanes][64 channels] of lane (mean, M2) -> the workgroup's Welford row
     float* red = (float*)ring;
     float* r1 = red + (wm * 32 + r32) * BN + wn * WN + 4 * h;
     float* r2 = r1 + 64 * BN;
+    const float nl = (float)(TM * ntile);  // values per lane and channel
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      *(f32x4*)(r1 + 8 * g) = f32x4{st1[4 * g], st1[4 * g + 1], st1[4 * g + 2], st1[4 * g + 3]};
-      *(f32x4*)(r2 + 8 * g) = f32x4{st2[4 * g], st2[4 * g + 1], st2[4 * g + 2], st2[4 * g + 3]};
+      float m[4], q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lane_stat_final(ls[4 * g + e], nl, &m[e], &q[e]);
+      *(f32x4*)(r1 + 8 * g) = f32x4{m[0], m[1], m[2], m[3]};
+      *(f32x4*)(r2 + 8 * g) = f32x4{q[0], q[1], q[2], q[3]};
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (tid < 2 * BN) {
-      const int q = tid / BN, col = tid - q * BN;
-      a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = col_sum(red + q * 64 * BN + col, 64, BN);
+    if (tid < BN) {
+      float mean, m2;
+      lane_rows_merge(red + tid, red + 64 * BN + tid, 64, BN, nl, &mean, &m2);
+      a.stats[((size_t)blockIdx.x * 2) * BN + tid] = mean;
+      a.stats[((size_t)blockIdx.x * 2 + 1) * BN + tid] = m2;
+      if (tid == 0) a.stats[(size_t)gridDim.x * 2 * BN + blockIdx.x] = (float)(TH * TW * ntile);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

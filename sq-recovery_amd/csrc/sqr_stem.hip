@@ -9,7 +9,7 @@
 // reduction and apply) plus once for the weight gradient.  Here it lives only in registers/LDS:
 //
 //   forward  S1 stem_stats_kernel : recompute conv1 per 8x32-pixel tile (MFMA, input window in
-//            LDS), per-block BN partials (sum x, sum x^2 of the bf16-rounded values)
+//            LDS), per-block BN partials (Welford rows: mean, M2 of the bf16-rounded values)
 //            finalize (sqr_bn.hip)  : batch mean / invstd, running stats, scale / shift
 //            S2 stem_pool_kernel  : recompute conv1 for a 4x16 pooled tile (+1 halo row / col),
 //            y = bf16(relu(bf16(x) * scale + shift)), 3x3/2 max-pool with torch's first-max tie
@@ -167,16 +167,18 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   V8<T> wf[4][2];
   load_wfrag<T>(w, lane, wf);
-  float s1[16], s2[16];
+  // per lane and channel: shifted sums of its values about its first one (sqr_common.h LaneStat)
+  LaneStat ls[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) s1[i] = s2[i] = 0.f;
+  for (int i = 0; i < 16; ++i) ls[i] = LaneStat{0.f, 0.f, 0.f};
   Window<TI, T, 22, 70> pf;
   auto fetch = [&](int t) {
     const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
     pf.load(img + (size_t)n * H * W, H, W, 16 * ty - 3, 64 * tx - 3);
   };
   if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  int mytiles = 0;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x, ++mytiles) {
     __syncthreads();  // previous tile's window reads are done
     pf.store(win);
     __syncthreads();
@@ -190,21 +192,24 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = rnd<T>(acc[jb][e]);
-          s1[jb * 4 + e] += v;
-          s2[jb * 4 + e] = fmaf(v, v, s2[jb * 4 + e]);
-        }
+        for (int e = 0; e < 4; ++e) lane_stat_add(ls[jb * 4 + e], rnd<T>(acc[jb][e]), t == (int)blockIdx.x && b == 0);
     }
   }
-  // reduce over the 16 pixel lanes (fixed xor tree), then over the 4 waves in order
+  // lane (mean, M2) over its 4 * mytiles values, merged over the 16 pixel lanes by an xor tree of
+  // equal-count pairs (both partners compute the same value), then over the 4 waves in order
+  float n = (float)(4 * mytiles), m[16], q[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 16; ++i) lane_stat_final(ls[i], n, &m[i], &q[i]);
 #pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-      s1[i] += __shfl_xor(s1[i], off, 64);
-      s2[i] += __shfl_xor(s2[i], off, 64);
+  for (int off = 1; off < 16; off <<= 1) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float mb = __shfl_xor(m[i], off, 64), qb = __shfl_xor(q[i], off, 64);
+      const float d = mb - m[i];
+      m[i] = (m[i] + mb) * 0.5f;
+      q[i] = (q[i] + qb) + d * d * (n * 0.5f);
     }
+    n *= 2.f;
   }
   __syncthreads();
   if (fr == 0) {
@@ -213,16 +218,17 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int c = 16 * jb + 4 * fq + e;
-        red[(wave * 2 + 0) * KC + c] = s1[jb * 4 + e];
-        red[(wave * 2 + 1) * KC + c] = s2[jb * 4 + e];
+        red[(wave * 2 + 0) * KC + c] = m[jb * 4 + e];
+        red[(wave * 2 + 1) * KC + c] = q[jb * 4 + e];
       }
   }
   __syncthreads();
-  if (tid < 2 * KC) {
-    const int q = tid / KC, c = tid - q * KC;
-    const float v = ((red[(0 * 2 + q) * KC + c] + red[(1 * 2 + q) * KC + c]) + red[(2 * 2 + q) * KC + c]) +
-                    red[(3 * 2 + q) * KC + c];
-    part[((size_t)blockIdx.x * 2 + q) * KC + c] = v;
+  if (tid < KC) {
+    float mean, m2;
+    lane_rows_merge(red + tid, red + KC + tid, 4, 2 * KC, n, &mean, &m2);
+    part[((size_t)blockIdx.x * 2) * KC + tid] = mean;
+    part[((size_t)blockIdx.x * 2 + 1) * KC + tid] = m2;
+    if (tid == 0) part[(size_t)gridDim.x * 2 * KC + blockIdx.x] = 4.f * n;
   }
 }
 
@@ -646,7 +652,7 @@ extern "C" int sqr_stem_fused_supported(int N, int H, int W) {
 extern "C" size_t sqr_stem_fused_workspace_bytes(int N, int H, int W) {
   StemGeom g;
   if (stem_geom(N, H, W, &g)) return 0;
-  const size_t fwd = a256((size_t)GRID_PERSIST * 2 * KC * 4) + a256(2 * KC * 4);
+  const size_t fwd = a256((size_t)GRID_PERSIST * (2 * KC + 1) * 4) + a256(2 * KC * 4);
   const size_t bwd = a256((size_t)GRID_PERSIST * PART_BWD * 4) + a256((size_t)PART_BWD * 8);
   return fwd > bwd ? fwd : bwd;
 }
@@ -704,7 +710,7 @@ extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int y_dtype, int N
   }
   hipStream_t st = as_stream(stream);
   float* part = (float*)workspace;
-  float* coef = (float*)((char*)workspace + a256((size_t)GRID_PERSIST * 2 * KC * 4));
+  float* coef = (float*)((char*)workspace + a256((size_t)GRID_PERSIST * (2 * KC + 1) * 4));
   if (training) {
     const int ntiles = N * (g.Hc / 8) * (g.Wc / 32);
     const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;

@@ -153,6 +153,15 @@ def _split(x):
     return x, None
 
 
+def partial_counts(stats):
+    """The per-row pixel counts that follow a [rows, 2, C] statistics-partials view in its buffer
+    (forward rows are Welford (mean, M2) pairs; sqr_bn_dev.h merge_stats_c)."""
+    base = stats._base if stats._base is not None else stats
+    rows, _, C = stats.shape
+    off = stats.storage_offset() - base.storage_offset()
+    return base.reshape(-1)[off + rows * 2 * C: off + rows * 2 * C + rows]
+
+
 def _check_stats(stats, x):
     if stats is not None:
         C = x.shape[1]

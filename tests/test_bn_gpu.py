@@ -120,7 +120,7 @@ def test_stem_eval_matches_torch():
 def test_conv_bn_stats_fused(cfg, dtype):
     """BN batch statistics taken from the conv epilogue partials (sqr_conv2d_fwd_stats ->
     sqr_bn_fwd_stats) == statistics reduced over the stored conv output (sqr_bn_fwd)."""
-    from sqr.bn import bn_act
+    from sqr.bn import bn_act, partial_counts
     from sqr.conv import conv2d
     N, C, K, H, R, s = cfg
     g = torch.Generator().manual_seed(N * C + H)
@@ -133,10 +133,14 @@ def test_conv_bn_stats_fused(cfg, dtype):
         assert torch.equal(y, y2)
         Ho = y.shape[2]
         assert st.shape[1:] == (2, K) and st.shape[0] * 64 >= N * Ho * Ho
+        # Welford rows (mean_t, M2_t) + per-row pixel counts (sqr.bn.partial_counts)
+        cnt = partial_counts(st).double()
+        assert int(cnt.sum()) == N * Ho * Ho
         yf = y.double()
-        ref_sum = yf.sum((0, 2, 3))
-        assert _rel(st.double().sum(0)[0], ref_sum) <= 1e-5
-        assert _rel(st.double().sum(0)[1], (yf * yf).sum((0, 2, 3))) <= 1e-5
+        mean = (cnt[:, None] * st[:, 0].double()).sum(0) / cnt.sum()
+        m2 = (st[:, 1].double() + cnt[:, None] * (st[:, 0].double() - mean) ** 2).sum(0)
+        assert _rel(mean, yf.mean((0, 2, 3))) <= 1e-5
+        assert _rel(m2, ((yf - yf.mean((0, 2, 3), keepdim=True)) ** 2).sum((0, 2, 3))) <= 1e-5
         a = bn_act((y, st), bn_a, relu=True)
         b = bn_act(y, bn_b, relu=True)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
@@ -162,12 +166,21 @@ def test_stem_stats_fused(dtype):
 
 
 def _partials(x, rows=3):
-    """[rows][2][C] f32 (sum, sum of squares) over disjoint pixel sets — what a stats-producing conv
-    epilogue hands the BatchNorm."""
+    """[rows][2][C] f32 Welford rows (mean, M2) over disjoint pixel sets, followed in memory by the
+    rows' pixel counts — what a stats-producing conv epilogue hands the BatchNorm."""
     N, C, H, W = x.shape
-    flat = x.detach().float().permute(0, 2, 3, 1).reshape(-1, C)
-    parts = [torch.stack([p.sum(0), (p * p).sum(0)]) for p in flat.chunk(rows)]
-    return torch.stack(parts).contiguous()
+    flat = x.detach().double().permute(0, 2, 3, 1).reshape(-1, C)
+    chunks = flat.chunk(rows)
+    parts = torch.stack([torch.stack([p.mean(0), ((p - p.mean(0)) ** 2).sum(0)]) for p in chunks]).float()
+    cnt = torch.tensor([float(p.shape[0]) for p in chunks])
+    buf = torch.cat([parts.reshape(-1), cnt])
+    return buf, len(chunks)
+
+
+def _stats_view(buf_rows, device):
+    buf, rows = buf_rows
+    b = buf.to(device)
+    return b[:b.numel() - rows].view(rows, 2, -1)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
@@ -202,8 +215,8 @@ def test_bn_add_act(cfg, dtype, training):
     cl = dict(memory_format=torch.channels_last)
     xag = xa.to(DEV).to(dtype).contiguous(**cl).requires_grad_(True)
     xbg = xb.to(DEV).to(dtype).contiguous(**cl).requires_grad_(True)
-    a_in = (xag, _partials(xa).to(DEV)) if training else xag
-    b_in = (xbg, _partials(xb, 5).to(DEV)) if training else xbg
+    a_in = (xag, _stats_view(_partials(xa), DEV)) if training else xag
+    b_in = (xbg, _stats_view(_partials(xb, 5), DEV)) if training else xbg
     y = bn_add_act(a_in, ga, b_in, gb, relu=relu)
     assert y.dtype == dtype and y.is_contiguous(**cl)
     y.backward(gy.to(DEV).to(dtype).contiguous(**cl))
@@ -219,3 +232,48 @@ def test_bn_add_act(cfg, dtype, training):
         assert _rel(m.running_mean, r.running_mean) <= 1e-6
         assert _rel(m.running_var, r.running_var) <= 1e-6
         assert int(m.num_batches_tracked) == int(r.num_batches_tracked)
+
+
+# ---------------------------------------------------------------- Welford-equivalent batch statistics
+# A channel with |mean| >> std: E[x^2] - mean^2 from fp32 partials would lose ~1e-3 of the variance at
+# mean 100, std ~1; the Welford rows (mean_t, M2_t) merged with Chan's formula keep it.  Checked on the
+# internal reduction (bn_act on a tensor), the implicit-GEMM conv epilogue (1x1), the tiled direct
+# conv (3x3, layers 2-4 shape) and the persistent layer-1 conv (3x3, 64 channels at 64x64): the conv
+# weights have only the centre tap so every output pixel (no border effect) is mean ~100, std ~1.25.
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("path", ["reduce", "conv1x1", "conv3x3_tiled", "conv3x3_layer1"])
+def test_bn_large_mean_welford(path, dtype):
+    from sqr.bn import bn_act
+    from sqr.conv import conv2d
+    if dtype == torch.float32 and path.startswith("conv3x3"):
+        pytest.skip("the direct 3x3 kernels are 16-bit; fp32 runs the implicit GEMM (conv1x1 covers it)")
+    # (the tiled kernel takes a grid of >= 128 tiles: layer-2 shape at batch 32; the persistent one two
+    # tiles per workgroup at batch 16)
+    N, C, H = {"reduce": (4, 64, 32), "conv1x1": (4, 64, 32), "conv3x3_tiled": (32, 128, 32),
+               "conv3x3_layer1": (16, 64, 64)}[path]
+    g = torch.Generator().manual_seed(100)
+    x = 1.0 + 0.1 * torch.randn(N, C, H, H, generator=g)
+    cl = dict(memory_format=torch.channels_last)
+    xg = x.to(DEV).to(dtype).contiguous(**cl)
+    bn = _bn(C, 3).to(DEV).train()
+    with torch.no_grad():
+        if path == "reduce":
+            y = (100.0 + torch.randn(N, C, H, H, generator=g)).to(DEV).to(dtype).contiguous(**cl)
+            out = bn_act(y, bn, relu=False)
+        else:
+            R = 1 if path == "conv1x1" else 3
+            w = torch.zeros(C, C, R, R)
+            w[:, :, R // 2, R // 2] = (100.0 / C) * (1 + 0.05 * torch.randn(C, C, generator=g))
+            y, st = conv2d(xg, w.to(DEV), None, 1, R // 2, stats=True)
+            out = bn_act((y, st), bn, relu=False)
+    torch.cuda.synchronize()
+    yd = y.double().cpu()
+    mean = yd.mean((0, 2, 3))
+    assert mean.min() > 80 and (yd.std((0, 2, 3)) < 3).all()  # the regime under test: |mean| >> std
+    ref = _bn(C, 3).double().train()
+    ref_out = ref(yd)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert _rel(out, ref_out) <= tol
+    # the statistics themselves, in every dtype (a cancelling E[x^2] - mean^2 misses these by ~1e-3)
+    assert _rel(bn.running_var, ref.running_var) <= 1e-5, _rel(bn.running_var, ref.running_var)
+    assert _rel(bn.running_mean, ref.running_mean) <= 1e-6

@@ -399,6 +399,9 @@ ACC_SHAPES = [
     (4, 128, 32, 128, 3, 1), (4, 256, 16, 256, 3, 1), (4, 512, 8, 512, 3, 1),
     (4, 64, 64, 128, 3, 2), (4, 128, 32, 256, 3, 2), (4, 256, 16, 512, 3, 2), (64, 64, 64, 128, 3, 2),
     (4, 64, 64, 128, 1, 2), (2, 64, 128, 64, 3, 1), (2, 64, 128, 128, 3, 2),
+    # 512x512 input at batch 16 (config 5's step test): several tiles per image row in the tiled
+    # 8-wave layer-2 kernel and the layer-3 stride-2 kernel
+    (16, 128, 64, 128, 3, 1), (16, 128, 64, 256, 3, 2), (16, 256, 32, 512, 3, 2), (16, 256, 32, 256, 3, 1),
 ]
 
 
@@ -436,7 +439,7 @@ def test_conv_bwd_data_acc(shape, dtype):
 # and the per-channel sums (sum g, sum g*(x - mean)) — the persistent layer-1 kernel (ring wrap at
 # the bench batch), the tiled kernels of layers 2-4, and the implicit-GEMM fallback (fp32, odd size).
 BNB_SHAPES = [(4, 64, 64, 64), (64, 64, 64, 64), (4, 128, 32, 128), (64, 128, 32, 128), (4, 256, 16, 256),
-              (4, 512, 8, 512), (2, 64, 128, 64), (3, 32, 20, 32)]
+              (4, 512, 8, 512), (2, 64, 128, 64), (3, 32, 20, 32), (16, 128, 64, 128), (16, 256, 32, 256)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=["bf16", "f16", "f32"])

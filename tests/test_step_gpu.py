@@ -43,12 +43,12 @@ def _rel_err(a, b):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("config,batch", [(2, 64), (4, 64), (5, 16)],
-                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B16"])
-def test_bench_step_gradients_vs_f64(config, batch):
+@pytest.mark.parametrize("config,batch,dtype", [(2, 64, None), (4, 64, None), (5, 16, None), (5, 16, torch.bfloat16)],
+                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B16", "cfg5shape_bf16_512_B16"])
+def test_bench_step_gradients_vs_f64(config, batch, dtype):
     import bench
     import ref_torch
-    tr = bench.Trainer(torch.device(DEV), config=config, batch=batch)
+    tr = bench.Trainer(torch.device(DEV), config=config, batch=batch, dtype=dtype)
     dt = tr.dtype
     tr.capture()
     assert tr.graph is not None
