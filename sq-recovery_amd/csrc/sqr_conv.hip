@@ -201,9 +201,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nkt) issue(s, s);
   if (nkt >= STAGES - 1) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
 
@@ -251,11 +251,12 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
       }
     }
-    // retire tile kt+1 (leave the younger tiles in flight), then let every wave see it
+    // retire tile kt+1 (leave the younger tiles in flight), then let every wave see it; lgkmcnt(0):
+    // this wave's reads of tile kt are done before the barrier after which tile kt's stage is refilled
     if (more) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
   }
@@ -487,9 +488,9 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nkt) issue(s, s);
   if (nkt >= STAGES - 1) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
 
@@ -557,9 +558,9 @@ __global__ void __launch_bounds__(256) conv_tn_kernel(TNArgs a) {
       }
     }
     if (more) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
   }

@@ -259,9 +259,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   for (int q = 0; q < PD; ++q) issue_w(q);
   // window 0 and weight tile 0 landed; tiles 1 .. PD-1 stay in flight
   if constexpr (PD == 2) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB) : "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
   }
   __builtin_amdgcn_s_barrier();
 
@@ -312,31 +312,36 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
       }
+      // Every step-end wait also retires this wave's own LDS reads (lgkmcnt(0)): the raw s_barrier
+      // does not wait for them on gfx950, and after it other waves DMA into the stage just read —
+      // an LDS-DMA write is not ordered behind another wave's queued ds_read, so a read still in
+      // the LDS queue could see the next tile (seen as a rare wrong 16-channel fragment at B = 16
+      // with two workgroups per CU; the epilogue's reuse of the LDS for statistics relies on it too)
       if constexpr (PD == 2) {
         const bool more = t < 7 || next;
         // retire the weight tile of the next step (and at tap 8 the next window, which is older);
         // at taps 0-1 the next chunk's window is younger than it and stays in flight
         if (!more) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         } else if (NWB == 2 && t <= 1 && next) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB + WP) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB + WP) : "memory");
         } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB) : "memory");
         }
       } else {
         // retire weight tile step+1 (issued at step+1-PD): younger are tiles step+2 .. step+PD and,
         // for t <= PD-1, this chunk's window load (issued at t = 0 after that step's tile load)
         if (t <= PD - 1) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1) + WP) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1) + WP) : "memory");
         } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
         }
       }
       __builtin_amdgcn_s_barrier();
     }
   }
   if constexpr (PD != 2) {  // drain the dummy loads before the epilogue reuses the LDS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
 
@@ -754,7 +759,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       if (tid == 0) a.stats[(size_t)gridDim.x * 2 * BN + blockIdx.x] = (float)(TH * TW * ntile);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   clock_end(a.tp);
 }
 
@@ -851,7 +856,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   };
 #pragma unroll
   for (int q = 0; q < PD; ++q) issue_w(q);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
   __builtin_amdgcn_s_barrier();
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -916,9 +921,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
         // it is younger than tile q+1, i.e. for the first PD-1 steps of the chunk)
         const int s = q - 9 * cc;
         if (next_win && s <= PD - 2)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1) + WP) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1) + WP) : "memory");
         else
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PB * (PD - 1)) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
         __builtin_amdgcn_s_barrier();
       }
     }
@@ -929,7 +934,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
   constexpr int SL = BN / 8, PX = 2 * TW, HALF = TH * PX * SL;
   static_assert(TH * PX * BN * 2 <= NWIN * WIN + STAGES * TILE_B, "staging tile fits the LDS");
   if (TH * PX * BN * 2 > NWIN * WIN) {  // staging overlaps the weight ring: its dummy tail loads first
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
   }
   static_assert(SL >= 8, "staging swizzle assumes at least 8 slots per pixel");
@@ -995,7 +1000,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail loads
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the dummy tail loads
   clock_end(a.tp);
 }
 

@@ -14,11 +14,12 @@
 //            S2 stem_pool_kernel  : recompute conv1 for a 4x16 pooled tile (+1 halo row / col),
 //            y = bf16(relu(bf16(x) * scale + shift)), 3x3/2 max-pool with torch's first-max tie
 //            rule -> pooled output (bf16) + argmax tap (u8)
-//   backward S3 stem_bwd_kernel   : per 4x32-pixel tile, recompute x, route the pooled gradient to
-//            its argmax pixel (g = dpool * [y > 0]), and accumulate over the whole batch
-//              T1[k][j] = sum_p g[p][k] A[p][j],  T2[k][j] = sum_p x[p][k] A[p][j],  T3[j] = sum_p A[p][j]
-//              sum_p g[p][k],  sum_p g[p][k] x[p][k]
-//            (A = the 7x7 input patch of pixel p, taps j = 8r + s padded to 64) with MFMA
+//   backward S3 stem_bwd_kernel   : per 4x32-pixel tile, route the pooled gradient to its argmax
+//            pixel (g = dpool * [y > 0]) and accumulate over the whole batch, with MFMA,
+//              T1[k][j] = sum_p g[p][k] A[p][j],  S[i][j] = sum_p A[p][i] A[p][j],  T3[j] = sum_p A[p][j],
+//              sum_p g[p][k]
+//            (A = the 7x7 input patch of pixel p, taps j = 8r + s padded to 64); x = W A is never
+//            recomputed: T2 = sum_p x A^T = W S and sum_p g x = rowsum(W o T1) in the finalize
 //            S4 colsum + stem_bwd_finalize_kernel: BN backward in closed form.  The reference's
 //              dx = a*g + k3*x + k2  (a = gamma*invstd, k3 = -a*invstd*dgamma/M, k2 = -a*sum g/M - k3*mean)
 //            is linear in (g, x, 1), so  dW = a*T1 + k3*T2 + k2*T3  and dgamma / dbeta follow from
@@ -49,7 +50,7 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 constexpr int KC = 64;           // conv1 output channels
 constexpr int WPITCH = 72;       // LDS window row pitch (elements): 144 B, a multiple of 4 B
 constexpr int GRID_PERSIST = 512;  // persistent grids (fixed: the partial-sum order is part of the result)
-constexpr int PART_BWD = 2 * KC * KC + 3 * KC;  // T1, T2, T3, sum g, sum g*x
+constexpr int PART_BWD = 2 * KC * KC + 2 * KC;  // T1, S (patch Gram matrix), T3, sum g
 
 template <typename T> struct TT;
 template <> struct TT<bf16> {
@@ -344,16 +345,21 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
 }
 
 // ---------------------------------------------------------------- S3: backward accumulation
-// tile = 4 conv rows x 32 conv cols = 128 pixels (8 blocks, 2 per wave); window 14 x 70 (2016 B,
-// padded to 2 KiB).  LDS images [64 rows][128 px] bf16 (256-B rows, XOR-swizzled 16-B slots, img_off):
-// AT[tap j][p] = A[p][j],  GT[k][p] = g,  XT[k][p] = x.  The conv1 weight fragments are kept in LDS
-// (8 KiB, read per conv block) so that two workgroups fit a CU's register file.
+// tile = 4 conv rows x 32 conv cols = 128 pixels; window 14 x 70 (2016 B, padded to 2 KiB).  LDS
+// images [64 rows][128 px] bf16 (256-B rows, XOR-swizzled 16-B slots, img_off):
+// AT[tap j][p] = A[p][j] (the 7x7 input patch of pixel p, taps padded to 64) and GT[k][p] = g.
+// The conv1 output x is NOT recomputed: every backward sum that involves it is linear in x = W A,
+//   T2[k][j] = sum_p x[p][k] A[p][j] = sum_i W[k][i] S[i][j],   S = sum_p A[p] A[p]^T (64 x 64)
+//   sum_p g[p][k] x[p][k] = sum_j W[k][j] T1[k][j]
+// so the kernel accumulates T1 = G^T A, the patch Gram matrix S = A^T A and T3 = column sums of A
+// (MFMA), and sum g; the finalize contracts them with the (16-bit) weights.  (x is then the f32
+// conv value rather than its bf16-rounded copy: a 2^-9-relative difference per element, averaged
+// over the batch, far inside the 16-bit tolerance of these gradients.)
 constexpr int S3_IMG = 64 * 256;
-constexpr int S3_WF = 8 * 64 * 16;
-constexpr int S3_LDS = 2048 + 3 * S3_IMG + S3_WF;
+constexpr int S3_LDS = 2048 + 2 * S3_IMG;
 
 // byte offset of element p of row: 16-B slot (p / 8) ^ key(row), key = (row & 15) ^ ((row >> 3) & 7) is
-// injective both on 16 consecutive rows (the MFMA fragment reads) and on rows 8 apart (the g / x
+// injective both on 16 consecutive rows (the MFMA fragment reads) and on rows 8 apart (the g
 // accesses of one pixel pair across a thread's 8 channels)
 __device__ __forceinline__ int img_off(int row, int p) {
   return row * 256 + ((((p >> 3) ^ ((row & 15) ^ ((row >> 3) & 7)))) << 4) + (p & 7) * 2;
@@ -385,14 +391,7 @@ __device__ __forceinline__ void pool_load(PoolIn& pi, const T* __restrict__ dpoo
 }
 
 template <typename TI, typename T>
-#ifndef SQR_STEM_BWD_OCC
-#define SQR_STEM_BWD_OCC 2  // workgroups per CU the backward's registers are sized for
-#endif
-#ifndef SQR_STEM_BWD_GRID
-#define SQR_STEM_BWD_GRID GRID_PERSIST  // persistent backward grid (<= GRID_PERSIST: workspace rows)
-#endif
-__global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const TI* __restrict__ img, const float* __restrict__ w,
-                                                          const T* __restrict__ dpool,
+__global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__ img, const T* __restrict__ dpool,
                                                           const T* __restrict__ ypool,
                                                           const uint8_t* __restrict__ argmax, int H, int W, int Hp,
                                                           int Wp, int tiles_x, int tiles_img, int ntiles,
@@ -401,28 +400,18 @@ __global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const T
   uint16_t* win = (uint16_t*)smem;
   char* AT = smem + 2048;
   char* GT = AT + S3_IMG;
-  char* XT = GT + S3_IMG;
-  V8<T>* WF = (V8<T>*)(XT + S3_IMG);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  if (wave == 0) {
-    V8<T> wf[4][2];
-    load_wfrag<T>(w, lane, wf);
+  f32x4 T1[4], S[4], T3 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) WF[(jb * 2 + ks) * 64 + lane] = wf[jb][ks];
-  }
-  f32x4 T1[4], T2[4], T3 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int jb = 0; jb < 4; ++jb) T1[jb] = T2[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int jb = 0; jb < 4; ++jb) T1[jb] = S[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
   V8<T> ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (T)1.f;
   // g items: thread = (quad = tid >> 3 of 2 x 16 quads, channel group cg = tid & 7)
   const int cg = tid & 7, quad = tid >> 3, qy = quad >> 4, qx = quad & 15;
-  float sg[8], sgx[8];
+  float sg[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) sg[e] = sgx[e] = 0.f;
+  for (int e = 0; e < 8; ++e) sg[e] = 0.f;
   const int oct = tid & 15;  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
 
   // register prefetch of the next tile's input window and pooled-gradient inputs
@@ -455,23 +444,7 @@ __global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const T
     }
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
-    // (a) x = conv1 (bf16-rounded) -> XT
-#pragma unroll 1
-    for (int b = 0; b < 2; ++b) {
-      const int p = (wave * 2 + b) * 16 + fr, py = p >> 5, px = p & 31;
-      V8<T> wf[4][2];
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) wf[jb][ks] = WF[(jb * 2 + ks) * 64 + lane];
-      f32x4 acc[4];
-      conv_block<T>((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
-#pragma unroll
-      for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) *(uint16_t*)(XT + img_off(16 * jb + 4 * fq + e, p)) = hbits<T>(acc[jb][e]);
-    }
-    // (b) A^T from the window
+    // (a) A^T from the window
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int j = (tid >> 4) + 16 * k, r = j >> 3, s = j & 7;
@@ -482,8 +455,7 @@ __global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const T
       for (int e = 0; e < 4; ++e) v[e] = (uint32_t)src[4 * e] | ((uint32_t)src[4 * e + 2] << 16);
       *(u32x4*)(AT + img_off(j, p0)) = v;
     }
-    __syncthreads();
-    // (c) g = pooled gradient routed to its argmax pixel: pixel (py, px) of quad (qy, qx) is tap
+    // (b) g = pooled gradient routed to its argmax pixel: pixel (py, px) of quad (qy, qx) is tap
     // (py - 2a + 1, px - 2b + 1) of pooling window (K + a, J + b), a, b in {0, 1}
 #pragma unroll
     for (int py = 0; py < 2; ++py) {
@@ -510,34 +482,31 @@ __global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const T
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = cg * 8 + e;
-        const uint32_t xx = *(const uint32_t*)(XT + img_off(c, p0));
-        const float g0 = g[0][e], g1 = g[1][e];
-        sg[e] += g0 + g1;
-        sgx[e] = fmaf(g0, plo<T>(xx), fmaf(g1, phi<T>(xx), sgx[e]));
-        *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)hbits<T>(g0) | ((uint32_t)hbits<T>(g1) << 16);
+        sg[e] += g[0][e] + g[1][e];
+        *(uint32_t*)(GT + img_off(c, p0)) = (uint32_t)hbits<T>(g[0][e]) | ((uint32_t)hbits<T>(g[1][e]) << 16);
       }
     }
     __syncthreads();
-    // (d) T1 += G^T A, T2 += X^T A over the tile's 128 pixels: wave w owns channels 16w .. 16w+15;
-    // T3 (column sums of A) for taps 16w .. 16w+15 with a ones operand
+    // (c) T1 += G^T A (wave w owns channels 16w .. 16w+15), S += A^T A (wave w owns taps 16w ..
+    // 16w+15 as rows), T3 += column sums of A (ones operand) over the tile's 128 pixels
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int p = 32 * ks + 8 * fq;
-      const int ch = 16 * wave + fr;
-      const V8<T> gfr = *(const V8<T>*)(GT + img_off(ch, p));
-      const V8<T> xfr = *(const V8<T>*)(XT + img_off(ch, p));
+      const int row = 16 * wave + fr;
+      const V8<T> gfr = *(const V8<T>*)(GT + img_off(row, p));
+      const V8<T> arow = *(const V8<T>*)(AT + img_off(row, p));
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) {
         const V8<T> afr = *(const V8<T>*)(AT + img_off(16 * jb + fr, p));
         T1[jb] = mfma(gfr, afr, T1[jb]);
-        T2[jb] = mfma(xfr, afr, T2[jb]);
+        S[jb] = mfma(arow, afr, S[jb]);
       }
       // (MFMA ignores EXEC: no lane-divergent branch around it)
-      T3 = mfma(ones, *(const V8<T>*)(AT + img_off(ch, p)), T3);
+      T3 = mfma(ones, arow, T3);
     }
   }
 
-  // ---- per-block partials: [T1 64x64][T2 64x64][T3 64][sum g 64][sum g x 64]
+  // ---- per-block partials: [T1 64x64][S 64x64][T3 64][sum g 64]
   float* out = part + (size_t)blockIdx.x * PART_BWD;
 #pragma unroll
   for (int jb = 0; jb < 4; ++jb)
@@ -545,26 +514,19 @@ __global__ void __launch_bounds__(256, SQR_STEM_BWD_OCC) stem_bwd_kernel(const T
     for (int e = 0; e < 4; ++e) {
       const int k = 16 * wave + 4 * fq + e, j = 16 * jb + fr;
       out[k * KC + j] = T1[jb][e];
-      out[KC * KC + k * KC + j] = T2[jb][e];
+      out[KC * KC + k * KC + j] = S[jb][e];
     }
   if (fq == 0) out[2 * KC * KC + 16 * wave + fr] = T3[0];  // every row of the ones-product is the column sum
   __syncthreads();
-  float* red = (float*)AT;  // [256][8] x 2 (spills into GT: both are consumed)
+  float* red = (float*)AT;  // [256][8]
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    red[tid * 8 + e] = sg[e];
-    red[2048 + tid * 8 + e] = sgx[e];
-  }
+  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = sg[e];
   __syncthreads();
   if (tid < 64) {  // channel c = tid: threads cg = c / 8 (quads 0..31), element e = c % 8
     const int c = tid, g8 = c >> 3, e = c & 7;
-    float a = 0.f, b = 0.f;
-    for (int qd = 0; qd < 32; ++qd) {
-      a += red[(qd * 8 + g8) * 8 + e];
-      b += red[2048 + (qd * 8 + g8) * 8 + e];
-    }
+    float a = 0.f;
+    for (int qd = 0; qd < 32; ++qd) a += red[(qd * 8 + g8) * 8 + e];
     out[2 * KC * KC + KC + c] = a;
-    out[2 * KC * KC + 2 * KC + c] = b;
   }
 }
 
@@ -596,22 +558,33 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
   }
 }
 
-// (b) block = output channel k, thread = tap j
+// (b) block = output channel k, thread = tap j (one wave): T2[k][j] = sum_i Wb[k][i] S[i][j] and
+// sum g x = sum_j Wb[k][j] T1[k][j] with Wb the 16-bit conv1 weights the forward used (zero on the
+// padding taps), then the closed-form BN backward
+template <typename T>
 __global__ void __launch_bounds__(64) stem_bwd_finalize_kernel(const double* __restrict__ tot, double M,
+                                                               const float* __restrict__ w,
                                                                const float* __restrict__ gamma,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ invstd, float* __restrict__ dw,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ double wk[KC];
   const int k = blockIdx.x, j = threadIdx.x;
-  const double t1 = tot[k * KC + j], t2 = tot[KC * KC + k * KC + j], t3 = tot[2 * KC * KC + j];
-  const double sg = tot[2 * KC * KC + KC + k], sgx = tot[2 * KC * KC + 2 * KC + k];
+  const int r = j >> 3, s = j & 7;
+  const bool real = r < 7 && s < 7;
+  wk[j] = real ? (double)(float)(T)w[k * 49 + r * 7 + s] : 0.0;
+  __syncthreads();
+  const double t1 = tot[k * KC + j], t3 = tot[2 * KC * KC + j];
+  double t2 = 0.0;
+  for (int i = 0; i < KC; ++i) t2 += wk[i] * tot[KC * KC + i * KC + j];
+  const double sg = tot[2 * KC * KC + KC + k];
+  const double sgx = wave_sum_d(wk[j] * t1);
   const double is = invstd[k], mu = mean[k];
   const double dgam = (sgx - mu * sg) * is;  // sum g * xhat
   const double a = (gamma ? (double)gamma[k] : 1.0) * is;
   const double k3 = -a * is * dgam / M;
   const double k2 = -a * sg / M - k3 * mu;
-  const int r = j >> 3, s = j & 7;
-  if (r < 7 && s < 7) dw[k * 49 + r * 7 + s] = (float)(a * t1 + k3 * t2 + k2 * t3);
+  if (real) dw[k * 49 + r * 7 + s] = (float)(a * t1 + k3 * t2 + k2 * t3);
   if (j == 0) {
     if (dgamma) dgamma[k] = (float)dgam;
     if (dbeta) dbeta[k] = (float)sg;
@@ -747,9 +720,9 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N
   hipStream_t st = as_stream(stream);
   float* part = (float*)workspace;
   const int tiles_x = g.Wc / 32, tiles_img = (g.Hc / 4) * tiles_x, ntiles = N * tiles_img;
-  const int grid = ntiles < SQR_STEM_BWD_GRID ? ntiles : SQR_STEM_BWD_GRID;
+  const int grid = ntiles < GRID_PERSIST ? ntiles : GRID_PERSIST;
   SQR_STEM_DISPATCH(x_dtype, y_dtype,
-                    hipLaunchKernelGGL((stem_bwd_kernel<TI, T>), dim3(grid), dim3(256), 0, st, (const TI*)x, w,
+                    hipLaunchKernelGGL((stem_bwd_kernel<TI, T>), dim3(grid), dim3(256), 0, st, (const TI*)x,
                                        (const T*)dy, (const T*)y, argmax, H, W, g.Hp, g.Wp, tiles_x, tiles_img, ntiles,
                                        part));
   SQR_HIP_LAUNCH_CHECK("stem_bwd_kernel");
@@ -757,8 +730,12 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N
   hipLaunchKernelGGL(colsum_kernel, dim3((PART_BWD + 31) / 32), dim3(256), 0, st, (const float*)part, grid, PART_BWD,
                      tot);
   SQR_HIP_LAUNCH_CHECK("colsum_kernel");
-  hipLaunchKernelGGL(stem_bwd_finalize_kernel, dim3(KC), dim3(64), 0, st, (const double*)tot,
-                     (double)N * g.Hc * g.Wc, gamma, save_mean, save_invstd, dw, dgamma, dbeta);
+  if (y_dtype == SQR_DTYPE_F16)
+    hipLaunchKernelGGL(stem_bwd_finalize_kernel<f16>, dim3(KC), dim3(64), 0, st, (const double*)tot,
+                       (double)N * g.Hc * g.Wc, w, gamma, save_mean, save_invstd, dw, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL(stem_bwd_finalize_kernel<bf16>, dim3(KC), dim3(64), 0, st, (const double*)tot,
+                       (double)N * g.Hc * g.Wc, w, gamma, save_mean, save_invstd, dw, dgamma, dbeta);
   SQR_HIP_LAUNCH_CHECK("stem_bwd_finalize_kernel");
   return 0;
 }

@@ -54,6 +54,16 @@ def _rel(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
 
 
+def _totals(st):
+    """(sum, sum of squares) per channel from a conv's forward-statistics partials: Welford rows
+    (mean_t, M2_t) and their pixel counts (sqr.bn.partial_counts) -> sum n_t mean_t and
+    sum (M2_t + n_t mean_t^2), float64."""
+    from sqr.bn import partial_counts
+    n = partial_counts(st).double()[:, None]
+    m, q = st[:, 0].double(), st[:, 1].double()
+    return torch.stack([(n * m).sum(0), (q + n * m * m).sum(0)])
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=["f32", "bf16", "f16"])
 @pytest.mark.parametrize("shape", RESNET + EXTRA, ids=lambda s: "N%dC%dH%dK%dR%ds%dp%d" % s)
 def test_conv_fwd_bwd(shape, dtype):
@@ -155,7 +165,7 @@ def test_conv3_direct(shape, dtype):
             y, st = sc.conv2d(xg, wg, None, 1, 1, stats=True)
             y.backward(gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last))
             torch.cuda.synchronize()
-            res[mode] = (y.float(), xg.grad.float(), st.double().sum(0), wg.grad.clone())
+            res[mode] = (y.float(), xg.grad.float(), _totals(st), wg.grad.clone())
     finally:
         lib().sqr_conv_set_direct(old)
     for mode in (2, 0):
@@ -192,7 +202,7 @@ def test_conv3_persistent_bands(N):
             y, st = sc.conv2d_fwd(x, krsc, d, stats=True)
             dx = sc.conv2d_bwd_data(gy, crsk, d)
             torch.cuda.synchronize()
-            res[mode] = (y.float(), st.double().sum(0), dx.float(), st.shape[0])
+            res[mode] = (y.float(), _totals(st), dx.float(), st.shape[0])
     finally:
         lib().sqr_conv_set_direct(old)
     y1, st1, dx1, rows1 = res[1]
@@ -277,8 +287,9 @@ def test_conv3p_bench_size_vs_f64(N, dtype):
     assert _rel(dx, dxr) <= tol
     assert _rel(dw, dwr) <= 2e-4
     yd = y.double().cpu()
-    assert _rel(st.double().sum(0)[0], yd.sum((0, 2, 3))) <= 1e-5
-    assert _rel(st.double().sum(0)[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
+    tot = _totals(st)
+    assert _rel(tot[0], yd.sum((0, 2, 3))) <= 1e-5
+    assert _rel(tot[1], (yd * yd).sum((0, 2, 3))) <= 1e-5
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])

@@ -8,7 +8,8 @@ step on the same images and the same 16-bit-rounded conv weights.  The tolerance
 guessed: a CPU float32 run that rounds to the compute dtype at the GPU step's storage points (conv
 operands and outputs, BatchNorm / pooled activations, and - through autograd of the casts - the
 activation gradients) measures how far a correct 16-bit step lands from float64; the GPU step must
-land as close (x3, with a small absolute floor for parameters whose gradient is ~0).
+land as close (L2 error x3, max error x5, with a small absolute floor for parameters whose
+gradient is ~0).
 """
 import numpy as np
 import pytest
@@ -42,6 +43,48 @@ def _rel_err(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
+def _l2_err(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+class _FixedLeaky(nn.Module):
+    """LeakyReLU whose branch per element is given (mask: True = identity) instead of decided by
+    the sign of its input."""
+
+    def __init__(self, mask, slope=0.01):
+        super().__init__()
+        self.mask, self.slope = mask, slope
+
+    def forward(self, x):
+        return torch.where(self.mask, x, self.slope * x)
+
+
+def _tail_masks(tr, sd, dt):
+    """The fc LeakyReLU branches the GPU step takes: its own layer4 output (an eager no-grad forward
+    from the same weights — every kernel is deterministic, so the captured step computes the same)
+    through the fp32-exact tail.  An fc pre-activation within rounding distance of 0 may take the
+    other branch than in float64; with 16 images per batch one such element moves a whole row of
+    fc.0's gradient, so the references take the GPU's branches (elsewhere they agree anyway)."""
+    feats = {}
+    blk = tr.net.encoder.layer4[1]
+    h = blk.register_forward_hook(lambda _m, _i, o: feats.__setitem__("f", o.detach().double().cpu()))
+    with torch.no_grad(), torch.autocast("cuda", dtype=dt):
+        tr.net(tr.images)
+    h.remove()
+    pool = feats["f"].mean((2, 3))
+    w0, b0 = sd["encoder.fc.0.weight"].double(), sd["encoder.fc.0.bias"].double()
+    w2, b2 = sd["encoder.fc.2.weight"].double(), sd["encoder.fc.2.bias"].double()
+    z0 = pool @ w0.T + b0
+    z2 = torch.where(z0 > 0, z0, 0.01 * z0) @ w2.T + b2
+    return z0 > 0, z2 > 0
+
+
+def _fix_tail(model, masks):
+    model.encoder.fc[1] = _FixedLeaky(masks[0])
+    model.encoder.fc[3] = _FixedLeaky(masks[1])
+    return model
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("config,batch,dtype", [(2, 64, None), (4, 64, None), (5, 16, None), (5, 16, torch.bfloat16)],
                          ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B16", "cfg5shape_bf16_512_B16"])
@@ -56,6 +99,7 @@ def test_bench_step_gradients_vs_f64(config, batch, dtype):
     # it runs with (fp16: gradients come out multiplied by it)
     sd = {k: v.detach().cpu().clone() for k, v in tr.net.state_dict().items()}
     scale = tr.scaler.get_scale() if tr.scaler is not None else 1.0
+    masks = _tail_masks(tr, sd, dt)
     tr.graph.replay()
     torch.cuda.synchronize()
     g_gpu = {n: p.grad.detach().double().cpu() / scale for n, p in tr.net.named_parameters()}
@@ -77,24 +121,31 @@ def test_bench_step_gradients_vs_f64(config, batch, dtype):
 
     ref64 = ref_torch.ResNetSQRef().double()
     ref64.load_state_dict(sd16)
-    loss64, g64 = run(ref64, images.double())
+    loss64, g64 = run(_fix_tail(ref64, masks), images.double())
     emu = ref_torch.ResNetSQRef()
     emu.load_state_dict(sd16)
+    _fix_tail(emu, masks)
     hooks = _emulated(emu, dt)
     loss_emu, g_emu = run(emu, images.to(dt).float(), scale)
     for h in hooks:
         h.remove()
 
     assert abs(loss_gpu - loss64) <= max(3 * abs(loss_emu - loss64), 1e-4 * abs(loss64)), (loss_gpu, loss_emu, loss64)
+    # Two error measures per parameter, each against the emulation's: the L2-relative error (x3) and
+    # the max-abs relative error (x5).  A ReLU input within rounding distance of 0 takes either
+    # branch in a correct 16-bit step; one such element moves one channel of a BatchNorm gradient,
+    # so the per-channel maximum is heavy-tailed (measured: cfg5 fp16 B=16 layer4.0.bn1.bias max
+    # ratio 3.7 with L2 ratio 1.1) while the L2 error of a correct step stays within ~2.5x.
     worst = []
     for n, b in g64.items():
-        e_gpu = _rel_err(g_gpu[n], b)
-        e_emu = _rel_err(g_emu[n], b)
-        worst.append((e_gpu / max(e_emu, 1e-4), n, e_gpu, e_emu))
+        e_gpu, e_emu = _rel_err(g_gpu[n], b), _rel_err(g_emu[n], b)
+        l_gpu, l_emu = _l2_err(g_gpu[n], b), _l2_err(g_emu[n], b)
+        worst.append((l_gpu / max(l_emu, 1e-4), n, l_gpu, l_emu, e_gpu, e_emu))
     worst.sort(reverse=True)
-    print("worst gpu/emulated error ratios:", ["%s %.2e/%.2e" % (n, a, b) for _, n, a, b in worst[:8]])
-    for _, n, e_gpu, e_emu in worst:
-        assert e_gpu <= 3 * e_emu + 1e-3, (n, e_gpu, e_emu)
+    print("worst gpu/emulated L2 (max) error:", ["%s %.2e/%.2e (%.2e/%.2e)" % w[1:] for w in worst[:8]])
+    for _, n, l_gpu, l_emu, e_gpu, e_emu in worst:
+        assert l_gpu <= 3 * l_emu + 1e-3, (n, "l2", l_gpu, l_emu)
+        assert e_gpu <= 5 * e_emu + 1e-3, (n, "max", e_gpu, e_emu)
     # the step then applied Adam: every parameter moved, by at most ~lr (Adam's first-order bound)
     for n, p in tr.net.named_parameters():
         delta = (p.detach().cpu() - sd[n]).abs().max().item()
