@@ -154,7 +154,11 @@ class Trainer:
         if probe_clock is not None:
             sconv.set_probe(*self.probe_key(), clock=probe_clock)
         try:
-            with torch.cuda.graph(graph):
+            # thread_local: ProcessGroupNCCL's watchdog thread polls the events of the eager warm-up
+            # all-reduces; under the default "global" mode such a poll from another thread during the
+            # capture is an unsafe call (hipErrorStreamCaptureUnsupported), the watchdog rethrows and the
+            # process aborts (tests/test_dp_graph_gpu.py)
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 self.static_loss = self.body()
         except Exception as e:  # N > 1 only: keep the run alive on eager DDP (reported in "dp")
             if self.gdp is None:
@@ -307,13 +311,35 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_quota():
+    """CPUs this job may use: the cgroup v2 quota (cpu.max "quota period"; the GPU box gives a job a
+    share of a large machine whose os.cpu_count() / affinity report every CPU), else the affinity."""
+    n = os.cpu_count() or 1
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:  # the job's declared thread budget
+        n = min(n, int(omp))
+    return n
+
+
 def cpu_baseline(images_cpu, params_cpu, state_dict, R, steps, cfg1_steps):
     """The reference's algorithm (oracle/ref_torch.py: stock torch CPU ops, f64 losses, Adam) timed
     on this host: config 2's workload (ImplicitLoss(R), the same batch) and config 1 (ExplicitLoss(32)
-    on the labels, B=4, fp32 network).  Thread count: BASELINE.md plans os.cpu_count(); the GPU box
-    exposes the whole machine's CPUs but runs this job on a share of them, so one timed step per
-    candidate count (16, 32, 64, ..., os.cpu_count()) picks the fastest, and every candidate's rate is
-    reported (thread_sweep) beside host_cpus."""
+    on the labels, B=4, fp32 network).  Thread count: BASELINE.md plans os.cpu_count(), but the GPU box
+    exposes the whole machine's CPUs while its cgroup quota gives this job a share of them (threads
+    beyond the quota only time-slice: a 256-thread step on a 16-CPU quota runs for minutes), so one
+    timed step per candidate count up to the quota (8, 16, 32, ..., quota) picks the fastest; every
+    candidate's rate is reported (thread_sweep) beside host_cpus and quota_cpus."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ref_torch
     ncpu = os.cpu_count() or 1
@@ -321,7 +347,8 @@ def cpu_baseline(images_cpu, params_cpu, state_dict, R, steps, cfg1_steps):
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = ncpu
-    cands = sorted({t for t in (16, 32, 64, 128, ncpu) if t <= ncpu} | {min(affinity, ncpu)})
+    quota = cpu_quota()
+    cands = sorted({t for t in (8, 16, 32, 64, 128) if t <= quota} | {quota})
 
     def make():
         net = ref_torch.ResNetSQRef()
@@ -334,20 +361,25 @@ def cpu_baseline(images_cpu, params_cpu, state_dict, R, steps, cfg1_steps):
         for _ in range(n):
             ref_torch.train_step(net, opt, crit, imgs, labels)
         secs = time.perf_counter() - t0
+        print("bench: cpu baseline %d step(s) of batch %d at %d threads: %.1f s" % (
+            n, imgs.shape[0], torch.get_num_threads(), secs), file=sys.stderr, flush=True)
         return imgs.shape[0] * n / secs, secs
 
     crit2 = ref_torch.ImplicitLossRef(R, 1.5, 260)
     net, opt = make()
+    torch.set_num_threads(quota)
     ref_torch.train_step(net, opt, crit2, images_cpu, None)  # warm-up
     sweep = {}
     for t in cands:
         torch.set_num_threads(t)
-        sweep[t] = timed(net, opt, crit2, images_cpu, None, 1)[0]
+        sweep[t], secs = timed(net, opt, crit2, images_cpu, None, 1)
+        if secs > 30:  # bounded sample: no slower candidates after a step this long
+            break
     best = max(sweep, key=sweep.get)
     torch.set_num_threads(best)
     v, secs = timed(net, opt, crit2, images_cpu, None, steps)
     out = {"value": v, "unit": "images/s", "cores": best, "kind": "port",
-           "host_cpus": ncpu, "affinity_cpus": affinity, "cpu_model": cpu_model(),
+           "host_cpus": ncpu, "affinity_cpus": affinity, "quota_cpus": quota, "cpu_model": cpu_model(),
            "thread_sweep": {str(k): round(x, 2) for k, x in sweep.items()},
            "sample": "%d timed train steps of batch %d after a warm-up step and a one-step thread sweep: "
                      "oracle/ref_torch.py ResNetSQ fp32 + reference-style f64 ImplicitLoss(R=%d), Adam, "

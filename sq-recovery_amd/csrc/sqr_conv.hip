@@ -711,6 +711,59 @@ __global__ void __launch_bounds__(256) wgrad_reduce_tc_kernel(const float* __res
   for (int i = t; i < 64 * RS; i += 256) dst[i] = outb[i];
 }
 
+// dw[i] = sum_z slab[z][i] for the slabs that are already in the gradient's KCRS order (the direct
+// weight-gradient kernel's; a 1x1 conv's TN slab [K][C] is too): a pure elementwise sum, read and
+// written in 16-B pieces with no transpose.  Block = QB quads x ZL split-lanes (QB * ZL = 256); lane
+// z sums splits z*NL .. z*NL+NL-1 with all NL loads in flight — indices past the last split are
+// clamped to it and their terms masked to zero, so no branch sits between the loads — then the ZL
+// lane sums are added in lane order through LDS.  The order depends only on the split count:
+// bitwise reproducible.  Workgroups past nred carry the riding BatchNorm work (wgrad_reduce_kernel).
+template <int NL>
+__global__ void __launch_bounds__(256) wgrad_sum_kernel(const float* __restrict__ slab, int splits, int zl_log2,
+                                                        long long E4, float* __restrict__ dw, int nred,
+                                                        bn::BnFinDev fin, bn::BnRedDev rj) {
+  extern __shared__ double ride_lds[];
+  if ((int)blockIdx.x >= nred) {
+    const int b = blockIdx.x - nred;
+    const int nfin = bn::fin_blocks(fin.C);
+    if (b < nfin) {
+      const int c = b * 4 + (int)(threadIdx.x >> 6);
+      if (c < fin.C)
+        bn::bn_bwd_finalize_w<float>(fin.part, fin.nblk, fin.M, fin.C, c, fin.gamma, fin.mean, fin.invstd, fin.dgamma,
+                                     fin.dbeta, fin.coef);
+    } else {
+      bn::bn_reduce_ride(rj, b - nfin, ride_lds);
+    }
+    return;
+  }
+  __shared__ f32x4 part[256];
+  const int QB = 256 >> zl_log2;
+  const int ql = threadIdx.x & (QB - 1), zl = threadIdx.x >> (8 - zl_log2);
+  const long long q = (long long)blockIdx.x * QB + ql;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (q < E4) {
+    const f32x4* __restrict__ src = (const f32x4*)slab + q;
+    const int z0 = zl * NL;
+    f32x4 v[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) v[u] = src[(size_t)min(z0 + u, splits - 1) * E4];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const float m = z0 + u < splits ? 1.f : 0.f;
+      acc += v[u] * m;
+    }
+  }
+  if (zl_log2 == 0) {
+    if (q < E4) ((f32x4*)dw)[q] = acc;
+    return;
+  }
+  part[threadIdx.x] = acc;  // [zl][ql]
+  __syncthreads();
+  if (zl != 0 || q >= E4) return;
+  for (int z = 1; z < (1 << zl_log2); ++z) acc += part[z * QB + ql];
+  ((f32x4*)dw)[q] = acc;
+}
+
 // ============================================================================ helpers
 // im2col for small-C inputs: col[m][kk] = x[n][oh*st-p+r][ow*st-p+s][c], kk=(r*S+s)*C+c, zero pad.
 // One thread per 8 consecutive kk of one row -> one 16-B (bf16) / 2x16-B (f32) store.
@@ -1054,6 +1107,37 @@ int reduce_zl_log2(int splits, int cap = 16) {
   int l = 0;
   while ((2 << l) <= cap && (2 << l) <= splits) ++l;
   return l;
+}
+
+// fixed-order sum of KCRS-ordered slabs (E floats each, E % 4 == 0): NL = loads per lane (the
+// next power of two >= splits, at most 16), ZL = lanes per quad (the next power of two >=
+// splits / 16)
+int launch_wgrad_sum(const float* slab, int splits, long long E, float* dw, hipStream_t st,
+                     const bn::BnFinDev* fin = nullptr, const bn::BnRedDev* red = nullptr, size_t red_lds = 0) {
+  bn::BnFinDev f = {};
+  bn::BnRedDev r = {};
+  if (fin) f = *fin;
+  if (red) r = *red;
+  const int nride = (fin ? bn::fin_blocks(fin->C) : 0) + (red ? red->nblk : 0);
+  const size_t lds = red ? red_lds : 0;
+  int nl = 1;
+  while (nl < splits && nl < 16) nl *= 2;
+  int zlg = 0;
+  while ((16 << zlg) < splits && zlg < 8) ++zlg;
+  SQR_CHECK_ARG(splits <= (16 << zlg), "wgrad_sum: %d splits", splits);
+  const long long E4 = E / 4;
+  const int QB = 256 >> zlg;
+  const int nred = (int)((E4 + QB - 1) / QB);
+  const dim3 grid(nred + nride), blk(256);
+  switch (nl) {
+    case 1: hipLaunchKernelGGL(wgrad_sum_kernel<1>, grid, blk, lds, st, slab, splits, zlg, E4, dw, nred, f, r); break;
+    case 2: hipLaunchKernelGGL(wgrad_sum_kernel<2>, grid, blk, lds, st, slab, splits, zlg, E4, dw, nred, f, r); break;
+    case 4: hipLaunchKernelGGL(wgrad_sum_kernel<4>, grid, blk, lds, st, slab, splits, zlg, E4, dw, nred, f, r); break;
+    case 8: hipLaunchKernelGGL(wgrad_sum_kernel<8>, grid, blk, lds, st, slab, splits, zlg, E4, dw, nred, f, r); break;
+    default: hipLaunchKernelGGL(wgrad_sum_kernel<16>, grid, blk, lds, st, slab, splits, zlg, E4, dw, nred, f, r); break;
+  }
+  SQR_HIP_LAUNCH_CHECK("wgrad_sum_kernel");
+  return 0;
 }
 
 // fixed-order split-K sum of the weight-gradient slabs into torch's [K][C][R][S]
@@ -1407,8 +1491,7 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
     const size_t avail = workspace_bytes - (size_t)(ws - (char*)workspace);
     rc = conv3w_launch(d->dtype, x, dy, (float*)ws, avail, d->N, d->H, d->W, d->C, d->K, &splits, st, d->stride);
     if (rc == 0) {
-      rc = launch_wgrad_reduce((const float*)ws, splits, d->K, Ng, d->C, d->R, d->S, d->C, 0, dw_kcrs, st, fin, red,
-                               red_lds);
+      rc = launch_wgrad_sum((const float*)ws, splits, (long long)d->K * d->C * 9, dw_kcrs, st, fin, red, red_lds);
       if (rc) return rc;
       return 0;
     }
@@ -1428,6 +1511,8 @@ static int bwd_weight_impl(const void* x, const void* col_in, const void* dy, fl
   if (d->dtype == SQR_DTYPE_F32) rc = launch_tn<float>(a, p, st);
   else SQR_DISPATCH16(d->dtype, T, rc = launch_tn<T>(a, p, st));
   if (rc) return rc;
+  if (!sh.im2col && d->R == 1 && d->S == 1)  // TN slab [K][C] = KCRS
+    return launch_wgrad_sum((const float*)ws, p.splits, (long long)d->K * d->C, dw_kcrs, st, fin, red, red_lds);
   return launch_wgrad_reduce((const float*)ws, p.splits, d->K, Ng, d->C, d->R, d->S, sh.im2col ? 1 : d->C,
                              (int)sh.im2col, dw_kcrs, st, fin, red, red_lds);
   return 0;

@@ -1012,7 +1012,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
 // MFMA fragments come from ds_read_b64_tr_b16 transposing reads.  Wave w owns channels
 // c0+16w..+15 for all 4 k-tiles and 9 taps: per 32-pixel k-step 4 dY + 9 X fragments feed
 // 36 MFMAs, and per chunk one window serves all 9 taps (the implicit-GEMM TN kernel re-gathers X
-// per tap).  Output: fp32 split slabs in the TN layout, reduced by wgrad_reduce_kernel.
+// per tap).  Output: fp32 split slabs in torch's KCRS layout, summed by wgrad_sum_kernel.
 // 32-B-window XOR key of an LDS pixel row by its (y, x) position in the tile/window:
 // the half-wave tr16 reads touch pixels (y, x..x+3) and (y, x+8..x+11) (TW >= 16) or
 // (y, x..x+3) and (y+1, x..x+3) (TW = 8); with 128-B rows the row parity (= x parity, widths are
@@ -1069,7 +1069,7 @@ constexpr int wg_lgkm(int j, int D, int NS, bool last) {
 struct D3WArgs {
   const void* x;   // [N][H][W][C]
   const void* dy;  // [N][Ho][Wo][K]
-  float* slab;     // [splits][K][9*C]
+  float* slab;     // [splits][K][C][9] (KCRS)
   int N, H, W, C, K, Ho, Wo;
   int tiles_x, chunks_per_img, nchunks, cps;  // cps = chunks per split
   int ntc, ntiles;                              // C/64, (K/64)*(C/64)
@@ -1324,16 +1324,41 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   }
 
 
-  // ---- epilogue: lane holds dW[k = k0+16kt+fr][tap t][c = c0+16w+4fq .. +3]
-  const size_t ng = (size_t)9 * a.C;
-  float* __restrict__ slab = a.slab + (size_t)split * a.K * ng;
-  const int c = c0 + 16 * wave + 4 * fq;
+  // ---- epilogue: the tile leaves in torch's KCRS order, slab[split][k][c][tap], so that the slabs
+  // sum elementwise into the gradient (wgrad_sum_kernel: coalesced, no transpose).  Lane (fr, fq) of
+  // wave w holds, for k = k0+16kt+fr, the 36 values (c = c0+16w+4fq+e, tap t): one contiguous 144-B
+  // run of the KCRS row dw[k][c0..c0+63][0..8].  The runs are staged in LDS (KG k-tiles of 16 rows
+  // per round; rows padded by 16 B so the 16 rows of a store start on different banks) and leave as
+  // whole 2304-B rows in 16-B pieces.
+  constexpr int RW = 64 * 9 + 4;  // staged row stride (floats)
+  constexpr int KG = STAGES * STAGE >= 64 * RW * 4 ? 4 : 2;
+  static_assert(STAGES * STAGE >= 16 * KG * RW * 4, "epilogue staging fits the pipeline's LDS");
+  __syncthreads();  // every wave is past its last fragment read of the pipeline stages
+  float* __restrict__ stg = (float*)smem;
+  float* __restrict__ slab = a.slab + ((size_t)split * a.K + k0) * a.C * 9 + (size_t)c0 * 9;
+  const size_t krow = (size_t)a.C * 9;
+  static_for<0, 4 / KG>([&](auto gc) __attribute__((always_inline)) {
+    constexpr int g = decltype(gc)::value * KG;
+    if constexpr (g > 0) __syncthreads();  // the previous round's rows have left
 #pragma unroll
-  for (int kt = 0; kt < 4; ++kt) {
-    float* row = slab + (size_t)(k0 + 16 * kt + fr) * ng + c;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) *(f32x4*)(row + t * a.C) = acc[t][kt];
-  }
+    for (int kq = 0; kq < KG; ++kq) {
+      float* dst = stg + (16 * kq + fr) * RW + (16 * wave + 4 * fq) * 9;
+      static_for<0, 9>([&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        f32x4 v;
+        v[0] = acc[(4 * j + 0) % 9][g + kq][(4 * j + 0) / 9];
+        v[1] = acc[(4 * j + 1) % 9][g + kq][(4 * j + 1) / 9];
+        v[2] = acc[(4 * j + 2) % 9][g + kq][(4 * j + 2) / 9];
+        v[3] = acc[(4 * j + 3) % 9][g + kq][(4 * j + 3) / 9];
+        *(f32x4*)(dst + 4 * j) = v;
+      });
+    }
+    __syncthreads();
+    for (int i = tid; i < 16 * KG * 144; i += 256) {
+      const int r = i / 144, q = i - r * 144;
+      *(f32x4*)(slab + (size_t)(16 * g + r) * krow + 4 * q) = *(const f32x4*)(stg + r * RW + 4 * q);
+    }
+  });
   clock_end(a.tp);
 }
 

@@ -168,9 +168,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,
                          int Wo, int K, int C, hipStream_t st, const void* addend = nullptr);
-// direct 3x3 / pad-1 / stride 1 or 2 bf16 weight gradient: fp32 slabs [splits][K][9*C] ((tap, c)
-// columns, the implicit-GEMM TN layout) for wgrad_reduce_kernel.  conv3w_slab_bytes = 0 if not
-// handled.  H, W: the input's size.
+// direct 3x3 / pad-1 / stride 1 or 2 bf16 weight gradient: fp32 slabs [splits][K][C][3][3] (torch's
+// KCRS order: the gradient is their elementwise sum, wgrad_sum_kernel).  conv3w_slab_bytes = 0 if
+// not handled.  H, W: the input's size.
 size_t conv3w_slab_bytes(int N, int H, int W, int C, int K, int stride = 1);
 int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t slab_bytes, int N, int H, int W, int C,
                   int K, int* splits, hipStream_t st, int stride = 1);

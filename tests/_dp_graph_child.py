@@ -70,7 +70,9 @@ def run(tmp_path):
         torch.cuda.current_stream().wait_stream(side)
         g = torch.cuda.CUDAGraph()
         b_opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(g):
+        # thread_local, as bench.py and sqr.step capture: the RCCL watchdog thread may poll the eager
+        # steps' all-reduce events while the capture is open
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             static = _body(b_net, b_opt, b_crit, x, gdp)
         for _ in range(2):
             g.replay()

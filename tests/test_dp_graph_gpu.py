@@ -22,5 +22,13 @@ def test_graph_dp_world1(tmp_path):
     env = dict(os.environ, NCCL_DEBUG="WARN")  # any RCCL complaint lands in the failure message
     r = subprocess.run([sys.executable, "-u", child, str(tmp_path)], capture_output=True, text=True, timeout=300,
                        env=env)
-    assert r.returncode == 0 and "DP_GRAPH_OK" in r.stdout and "DP_TEARDOWN_OK" in r.stdout, (
-        r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    ok = r.returncode == 0 and "DP_GRAPH_OK" in r.stdout and "DP_TEARDOWN_OK" in r.stdout
+    if not ok:
+        # the error text first (a watchdog exception's what() line), then the raw streams in full
+        key = [ln for ln in (r.stdout + r.stderr).splitlines()
+               if any(w in ln for w in ("what()", "Exception", "Error", "error", "DP_"))
+               and "NCCL WARN" not in ln]
+        print("\n".join(key))
+        print(r.stdout)
+        print(r.stderr)
+    assert ok, (r.returncode, key[:20])
