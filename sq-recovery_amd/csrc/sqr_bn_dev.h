@@ -250,6 +250,30 @@ __device__ __forceinline__ void merge_stats_w(const P* __restrict__ part, int nb
                                               double* mean_out, double* m2_out) {
   const int l = threadIdx.x & 63;
   const P* __restrict__ cnt = part + (size_t)nblk * 2 * C;
+  constexpr int RMAX = 8;  // rows per lane held in registers: one round of loads for nblk <= 512
+  if (nblk <= 64 * RMAX) {
+    double n[RMAX], mu[RMAX], q[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {  // branch-free: rows past nblk re-read row 0 and count 0
+      const int k = l + 64 * r, kk = k < nblk ? k : 0;
+      n[r] = k < nblk ? (double)cnt[kk] : 0.0;
+      mu[r] = (double)part[(size_t)kk * 2 * C + c];
+      q[r] = k < nblk ? (double)part[(size_t)kk * 2 * C + C + c] : 0.0;
+    }
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) a += n[r] * mu[r];
+    const double mean = wave_sum_d(a) / M;
+    double b = 0.0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const double d = mu[r] - mean;
+      b += q[r] + n[r] * d * d;
+    }
+    *mean_out = mean;
+    *m2_out = wave_sum_d(b);
+    return;
+  }
   double a = 0.0;
 #pragma unroll 4
   for (int k = l; k < nblk; k += 64) a += (double)cnt[k] * (double)part[(size_t)k * 2 * C + c];

@@ -290,10 +290,12 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
   if (a.stats) {
     // fused BatchNorm statistics of the STORED (dtype-rounded) output: this M-tile's Welford row
     // (mean, M2) per channel -> stats[tile_m][0/1][n] and its pixel count after the ntm rows (the BN
-    // layer finalizes from these partials instead of re-reading the whole activation).  Lanes: shifted
-    // sums of their valid pixels (sqr_common.h LaneStat), merged over the 16 pixel lanes by an xor
-    // tree and over the WAVES_M wave rows in order, both with Chan's formula (counts may differ in a
-    // partial last tile).
+    // layer finalizes from these partials instead of re-reading the whole activation).  The 16 lanes
+    // of a quarter-wave (same fq: the same 4 channels, 16 pixels per i) shift by the group's first
+    // value K (lane fr = 0, i = 0: the group's smallest pixel, valid whenever any of its pixels is),
+    // add their shifted values / squares / counts as plain floats over an xor tree (no division per
+    // level), and the group rows (n, mean = K + S/n, M2 = Q - S^2/n) of the WAVES_M wave rows are
+    // merged per column in a fixed order with Chan's formula (counts differ in a partial last tile).
     float* red = (float*)smem;  // [WAVES_M][BN][3]; the k loop ended with a barrier
     auto chan = [](float& n, float& m, float& q, float nb, float mb, float qb) {
       const float nn = n + nb;
@@ -307,41 +309,49 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
       q = q + qb + d * d * (n * nb / nn);
       n = nn;
     };
+    float vf[TM];  // 1 for this lane's valid pixels, 0 past the end of M
+    float nl = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      vf[i] = m0 + wm * WM + 16 * i + fr < g.M ? 1.f : 0.f;
+      nl += vf[i];
+    }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) nl += __shfl_xor(nl, off, 64);  // the group's count
+    const float inv_n = nl > 0.f ? 1.f / nl : 0.f;
+    const int lead = lane & 48;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      float cn[4], cm[4], cq[4];
+      float cm[4], cq[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        LaneStat ls = {0.f, 0.f, 0.f};
-        float n = 0.f;
+        float v[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) v[i] = (float)(T)acc[j][i][e];
+        const float K = __shfl(v[0], lead, 64);
+        float sa = 0.f, sq = 0.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const int m = m0 + wm * WM + 16 * i + fr;
-          if (m < g.M) {
-            lane_stat_add(ls, (float)(T)acc[j][i][e], n == 0.f);
-            n += 1.f;
-          }
-        }
-        cn[e] = n;
-        if (n > 0.f) {
-          lane_stat_final(ls, n, &cm[e], &cq[e]);
-        } else {
-          cm[e] = cq[e] = 0.f;
+          const float d = (v[i] - K) * vf[i];
+          sa += d;
+          sq = fmaf(d, d, sq);
         }
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
-          const float nb = __shfl_xor(cn[e], off, 64), mb = __shfl_xor(cm[e], off, 64),
-                      qb = __shfl_xor(cq[e], off, 64);
-          chan(cn[e], cm[e], cq[e], nb, mb, qb);
+          sa += __shfl_xor(sa, off, 64);
+          sq += __shfl_xor(sq, off, 64);
         }
+        const float sn = sa * inv_n;
+        cm[e] = K + sn;
+        cq[e] = fmaxf(sq - sa * sn, 0.f);
       }
       if (fr == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int col = wn * WN + 16 * j + 4 * fq + e;
-          red[(wm * BN + col) * 3] = cn[e];
-          red[(wm * BN + col) * 3 + 1] = cm[e];
-          red[(wm * BN + col) * 3 + 2] = cq[e];
+          red[(wm * BN + col) * 3] = nl;
+          red[(wm * BN + col) * 3 + 1] = nl > 0.f ? cm[e] : 0.f;
+          red[(wm * BN + col) * 3 + 2] = nl > 0.f ? cq[e] : 0.f;
         }
       }
     }
@@ -746,7 +756,8 @@ __global__ void __launch_bounds__(256) wgrad_sum_kernel(const float* __restrict_
     const int z0 = zl * NL;
     f32x4 v[NL];
 #pragma unroll
-    for (int u = 0; u < NL; ++u) v[u] = src[(size_t)min(z0 + u, splits - 1) * E4];
+    for (int u = 0; u < NL; ++u)  // nontemporal: the slabs are read once (tools/sum_bench.hip: -1.1 us)
+      v[u] = __builtin_nontemporal_load(src + (size_t)min(z0 + u, splits - 1) * E4);
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
       const float m = z0 + u < splits ? 1.f : 0.f;
@@ -1185,6 +1196,11 @@ extern "C" int sqr_conv2d_out_hw(const sqr_conv_desc* d, int* Ho, int* Wo) {
 static bool direct3(const sqr_conv_desc* d, const Shape& sh) {
   return !sh.im2col && d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->stride == 1 && d->pad == 1;
 }
+// the direct forward kernel's stride-2 mode (the first conv of layers 2-4)
+static bool direct3s2(const sqr_conv_desc* d, const Shape& sh) {
+  return !sh.im2col && d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->stride == 2 && d->pad == 1 &&
+         d->H == 2 * sh.Ho && d->W == 2 * sh.Wo;
+}
 // the direct weight-gradient kernel also takes stride 2 (the first conv of layers 2-4)
 static bool direct3w(const sqr_conv_desc* d, const Shape& sh) {
   return !sh.im2col && d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && (d->stride == 1 || d->stride == 2) &&
@@ -1256,6 +1272,11 @@ static int conv_fwd_impl(const void* x, const void* w_krsc, void* y, const sqr_c
   if (direct3(d, sh)) {
     rc = conv3_launch(d->dtype, x, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, st);
     if (rc != kNotHandled) return rc;  // launched (0) or failed; else the shape is not covered
+  }
+  if (direct3s2(d, sh)) {
+    rc = conv3_launch(d->dtype, x, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, st, nullptr,
+                      nullptr, 2);
+    if (rc != kNotHandled) return rc;
   }
   a.stats = stats;
   if (stats_rows) {  // one partial row per M tile of the config launch_nt will pick

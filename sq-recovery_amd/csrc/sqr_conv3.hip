@@ -38,7 +38,8 @@ struct D3Args {
   const uint8_t* bn_mask;  //      batch mean: out = conv * mask, stats = (sum g, sum g*(x - mean))
   const float* bn_mean;
   float* stats;     // nullable: BatchNorm partials [ntm][2][Nout]
-  int N, H, W, Cin, Nout;
+  int N, H, W, Cin, Nout;  // H, W: the OUTPUT size
+  int iH, iW;              // the input size (= H, W at stride 1; 2H, 2W at stride 2)
   int tiles_x, tiles_per_img;
   int ntm, ntn;
   int flip;
@@ -90,36 +91,55 @@ __device__ __forceinline__ void stats_reduce(const float (*s1)[4], const float (
 }
 
 // Forward BatchNorm statistics of a BM x BN output tile held as acc[j][i], from the 16-bit values
-// actually stored: the tile's Welford row (mean, M2) per channel (sqr_common.h LaneStat): each lane
-// has TM values of each of its channels (pixels 16i+fr), shifted about its first one; the
-// WAVES_M*16 lane entries of a column go through the same LDS transpose and are merged by one
-// thread per column.  Row count BM (written once per tile row by the tile_n = 0 workgroup).
+// actually stored: the tile's Welford row (mean, M2) per channel.  The 16 lanes of a quarter-wave
+// (same fq: the same 4 channels, 16 pixel rows of TM values each) shift by the group's first value K
+// (lane fr = 0, value 0: broadcast), add their shifted values and squares as plain floats over an xor
+// tree and leave (mean = K + S/n, M2 = Q - S^2/n) for n = 16 TM values — no cancellation while the
+// values stay within a few std of K, no per-level division; the WAVES_M group rows of a column are
+// merged by one thread in a fixed order (lane_rows_merge, float64).  Row count BM (written once per
+// tile row by the tile_n = 0 workgroup).
 template <typename T, int BN, int WAVES_M, int WAVES_N, int TM, int TN, int NT>
 __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* red, int wm, int wn, int fr, int fq,
                                            int tid, float* stats_row0, float* stats_row1, float* count, float bm) {
-  constexpr int WN = BN / WAVES_N, R = WAVES_M * 16;
-  float* r1 = red + (wm * 16 + fr) * BN + wn * WN + 4 * fq;
-  float* r2 = r1 + R * BN;
+  constexpr int WN = BN / WAVES_N;
+  constexpr float NG = 16.f * TM, INV_NG = 1.f / (16.f * TM);
+  const int lane = tid & 63, lead = lane & 48;
+  float* r1 = red + wm * BN + wn * WN + 4 * fq;
+  float* r2 = r1 + WAVES_M * BN;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     float m[4], q[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      LaneStat a = {0.f, 0.f, 0.f};
+      float v[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) v[i] = (e & 1) ? hi2f<T>(pk[j][i][e >> 1]) : lo2f<T>(pk[j][i][e >> 1]);
+      const float K = __shfl(v[0], lead, 64);
+      float sa = 0.f, sq = 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const uint32_t p = pk[j][i][e >> 1];
-        lane_stat_add(a, (e & 1) ? hi2f<T>(p) : lo2f<T>(p), i == 0);
+        const float d = v[i] - K;
+        sa += d;
+        sq = fmaf(d, d, sq);
       }
-      lane_stat_final(a, (float)TM, &m[e], &q[e]);
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        sa += __shfl_xor(sa, off, 64);
+        sq += __shfl_xor(sq, off, 64);
+      }
+      const float sn = sa * INV_NG;
+      m[e] = K + sn;
+      q[e] = fmaxf(sq - sa * sn, 0.f);
     }
-    *(f32x4*)(r1 + 16 * j) = f32x4{m[0], m[1], m[2], m[3]};
-    *(f32x4*)(r2 + 16 * j) = f32x4{q[0], q[1], q[2], q[3]};
+    if (fr == 0) {
+      *(f32x4*)(r1 + 16 * j) = f32x4{m[0], m[1], m[2], m[3]};
+      *(f32x4*)(r2 + 16 * j) = f32x4{q[0], q[1], q[2], q[3]};
+    }
   }
   __syncthreads();
   for (int col = tid; col < BN; col += NT) {
     float mean, m2;
-    lane_rows_merge(red + col, red + R * BN + col, R, BN, (float)TM, &mean, &m2);
+    lane_rows_merge(red + col, red + WAVES_M * BN + col, WAVES_M, BN, NG, &mean, &m2);
     stats_row0[col] = mean;
     stats_row1[col] = m2;
   }
@@ -136,14 +156,23 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 // BNB (backward-data into a BatchNorm+ReLU backward): x and the mask bits at the lane's outputs are
 // loaded before the main loop like ACC's addend; the stored value is g = conv * mask and the tile's
 // partial row of a.stats gets the BatchNorm backward sums (sum g, sum g*(x - mean)).
+// S = 2 (forward of a 3x3 / stride-2 / pad-1 conv, IMGS = 1, no flip): the (2TH+1) x (2TW+1) input
+// window of a TH x TW output tile is staged as four phase planes (a, b) = (input row, column parity
+// relative to the window origin), each TW+1 pixels wide (plane (., 1) has one unused column), plane
+// (a, .) holding TH+1-a rows.  Tap (r, c) of output pixel (y, x) reads plane (r & 1, c & 1) at
+// (y + (r >> 1), x + (c >> 1)): consecutive output pixels are consecutive plane rows and the tap
+// offset is one constant per tap, so the stride-1 fragment reads carry over unchanged.
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2,
-          bool ACC = false, bool BNB = false>
+          bool ACC = false, bool BNB = false, int S = 1>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
   constexpr int ROWB = 128, STAGES = PD + 1;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int WWID = TW + 2, WRI = (TH + 2) * WWID, WR = IMGS * WRI;  // halo window rows
+  static_assert(S == 1 || (S == 2 && IMGS == 1 && !ACC && !BNB), "stride 2: forward, one image per tile");
+  constexpr int WWID = S == 1 ? TW + 2 : TW + 1;
+  constexpr int P0 = (TH + 1) * WWID, P1 = TH * WWID;  // stride 2: rows of an a = 0 / a = 1 plane
+  constexpr int WRI = S == 1 ? (TH + 2) * WWID : 2 * P0 + 2 * P1, WR = IMGS * WRI;  // halo window rows
   constexpr int WROWS = (WR + 8 * NW - 1) / (8 * NW) * (8 * NW);
   constexpr int PB = BN / (8 * NW);                          // weight pieces per wave per step
   constexpr int WP = WROWS / (8 * NW);                       // window pieces per wave per chunk
@@ -204,10 +233,23 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     const int r = (i * NW + wave) * 8 + prow;  // window row
     const int ls = pslot ^ d3key(r);      // logical 16-B channel slot this lane fetches
     const int ii = r / WRI, rr = r - ii * WRI;     // image of the tile, row in its window
-    const int wy = rr / WWID, wx = rr - wy * WWID;  // constant divisors
-    const int h = h0 - 1 + wy, w = w0 - 1 + wx;
-    const bool ok = r < WR && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-    wvoff[i] = ok ? (uint32_t)(((((img + ii) * a.H + h) * a.W + w) * a.Cin) * 2 + ls * 16) : kOOB;
+    int h, w;
+    bool used = r < WR;
+    if constexpr (S == 1) {
+      const int wy = rr / WWID, wx = rr - wy * WWID;  // constant divisors
+      h = h0 - 1 + wy;
+      w = w0 - 1 + wx;
+    } else {  // plane (pa, pb) row (py, px) <- input (2h0 - 1 + 2py + pa, 2w0 - 1 + 2px + pb)
+      const int pa = rr >= 2 * P0 ? 1 : 0;
+      const int pb = pa ? (rr >= 2 * P0 + P1 ? 1 : 0) : (rr >= P0 ? 1 : 0);
+      const int pr = rr - (pa ? 2 * P0 + pb * P1 : pb * P0);
+      const int py = pr / WWID, px = pr - py * WWID;
+      h = 2 * h0 - 1 + 2 * py + pa;
+      w = 2 * w0 - 1 + 2 * px + pb;
+      used = used && (pb == 0 || px < TW);
+    }
+    const bool ok = used && (unsigned)h < (unsigned)a.iH && (unsigned)w < (unsigned)a.iW;
+    wvoff[i] = ok ? (uint32_t)(((((img + ii) * a.iH + h) * a.iW + w) * a.Cin) * 2 + ls * 16) : kOOB;
   }
   uint32_t bvoff[PB];
 #pragma unroll
@@ -290,7 +332,12 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
                              __builtin_amdgcn_readfirstlane((next ? cc + 1 : cc) * 128), wave);
       }
       const int r = t / 3, c3 = t % 3;
-      const int toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
+      int toff;
+      if constexpr (S == 1) {
+        toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
+      } else {
+        toff = ((r & 1) ? 2 * P0 + (c3 & 1) * P1 : (c3 & 1) * P0) + (r >> 1) * WWID + (c3 >> 1);
+      }
       const char* bst = bring + (PD == 2 ? (t % 3) : (step % STAGES)) * TILE_B;
       int qoff[TM];
 #pragma unroll
@@ -534,7 +581,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // 32x32x16 operand lanes: row r32 = lane & 31 (pixel / output channel), k half h = lane >> 5
   const int flip = a.flip;
   // BatchNorm statistics (this lane: pixel column, 16 channels wn*32 + 8g + 4h + e) over all tiles:
-  // shifted sums about the lane's first value of each channel (sqr_common.h LaneStat)
+  // sums of the values shifted by K = the channel's first value in pixel lane r32 = 0 (broadcast at
+  // tile 0, shared by the wave's 32 pixel lanes of that channel, so their sums add exactly in the
+  // final xor tree; no cancellation while the values stay within a few std of K)
   LaneStat ls[STATS ? 16 : 1];
 #pragma unroll
   for (int e = 0; e < (STATS ? 16 : 1); ++e) ls[e] = LaneStat{0.f, 0.f, 0.f};
@@ -683,12 +732,27 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       for (int g = 0; g < 4; ++g) {
         pk[i][g][0] = pack2<T>(acc[i][4 * g], acc[i][4 * g + 1]);
         pk[i][g][1] = pack2<T>(acc[i][4 * g + 2], acc[i][4 * g + 3]);
-#pragma unroll
-        for (int q = 0; q < 2 * STATS; ++q) {
-          lane_stat_add(ls[4 * g + 2 * q], lo2f<T>(pk[i][g][q]), k == 0 && i == 0);
-          lane_stat_add(ls[4 * g + 2 * q + 1], hi2f<T>(pk[i][g][q]), k == 0 && i == 0);
-        }
       }
+    if constexpr (STATS) {
+      if (k == 0) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            ls[4 * g + 2 * q].k = __shfl(lo2f<T>(pk[0][g][q]), lane & 32, 64);
+            ls[4 * g + 2 * q + 1].k = __shfl(hi2f<T>(pk[0][g][q]), lane & 32, 64);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            lane_stat_add(ls[4 * g + 2 * q], lo2f<T>(pk[i][g][q]), false);
+            lane_stat_add(ls[4 * g + 2 * q + 1], hi2f<T>(pk[i][g][q]), false);
+          }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // all waves are done with tile k's rows and the staging area
 #pragma unroll
@@ -736,24 +800,36 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = col_sum(red + sl * 16 + 8 * q + e, NT / 8, 8 * 16);
     }
   }
-  if constexpr (STATS) {  // red[2][64 pixel lanes][64 channels] of lane (mean, M2) -> the workgroup's Welford row
+  if constexpr (STATS) {  // xor tree over the 32 pixel lanes -> red[2][WAVES_M][64 channels] -> Welford row
     float* red = (float*)ring;
-    float* r1 = red + (wm * 32 + r32) * BN + wn * WN + 4 * h;
-    float* r2 = r1 + 64 * BN;
-    const float nl = (float)(TM * ntile);  // values per lane and channel
+    const float ng = (float)(32 * TM * ntile);  // values per wave and channel
+    const float inv = 1.f / ng;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       float m[4], q[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) lane_stat_final(ls[4 * g + e], nl, &m[e], &q[e]);
-      *(f32x4*)(r1 + 8 * g) = f32x4{m[0], m[1], m[2], m[3]};
-      *(f32x4*)(r2 + 8 * g) = f32x4{q[0], q[1], q[2], q[3]};
+      for (int e = 0; e < 4; ++e) {
+        float sa = ls[4 * g + e].s, sq = ls[4 * g + e].q;
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) {
+          sa += __shfl_xor(sa, off, 64);
+          sq += __shfl_xor(sq, off, 64);
+        }
+        const float sn = sa * inv;
+        m[e] = ls[4 * g + e].k + sn;
+        q[e] = fmaxf(sq - sa * sn, 0.f);
+      }
+      if (r32 == 0) {
+        float* r1 = red + wm * BN + wn * WN + 8 * g + 4 * h;
+        *(f32x4*)r1 = f32x4{m[0], m[1], m[2], m[3]};
+        *(f32x4*)(r1 + WAVES_M * BN) = f32x4{q[0], q[1], q[2], q[3]};
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (tid < BN) {
       float mean, m2;
-      lane_rows_merge(red + tid, red + 64 * BN + tid, 64, BN, nl, &mean, &m2);
+      lane_rows_merge(red + tid, red + WAVES_M * BN + tid, WAVES_M, BN, ng, &mean, &m2);
       a.stats[((size_t)blockIdx.x * 2) * BN + tid] = mean;
       a.stats[((size_t)blockIdx.x * 2 + 1) * BN + tid] = m2;
       if (tid == 0) a.stats[(size_t)gridDim.x * 2 * BN + blockIdx.x] = (float)(TH * TW * ntile);
@@ -1478,9 +1554,74 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
 
 
 // kNotHandled = not applicable (caller falls back to the implicit-GEMM path), 0 = launched, else error
+// stride-2 forward tiles (output TH x TW, one image per tile; the four-plane window and the 3-stage
+// weight ring fit 160 KiB): layer 2 (Cin 64: one window), layers 3-4 (Cin 128 / 256: two windows)
+namespace {
+struct D3S2FCfg {
+  int id, BM, BN, threads, TW, TH, nwb;
+};
+bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
+  const int nch = Cin / 64;
+  const D3S2FCfg cands[] = {
+      // id BM   BN  thr  TW  TH nwb
+      {0, 128, 128, 512, 32, 4, 1},  // Cin 64, Wo 32 (layer 2; 512x512: Wo 64)
+      {1, 64, 128, 256, 16, 4, 2},   // Wo 16 (layer 3; 512x512: layer 3 at Wo 32)
+      {2, 64, 128, 256, 8, 8, 2},    // Wo 8 (layer 4; 512x512: Wo 16)
+  };
+  for (const D3S2FCfg& c : cands) {
+    if ((c.nwb == 1) != (nch == 1)) continue;
+    if (Nout % c.BN || Wo % c.TW || Ho % c.TH) continue;
+    if ((long long)N * (Ho / c.TH) * (Wo / c.TW) * (Nout / c.BN) < 128 && g_direct < 2) continue;
+    *out = c;
+    return true;
+  }
+  return false;
+}
+}  // namespace
+
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
-                 float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb) {
+                 float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb, int stride) {
   if (g_direct == 0) return kNotHandled;
+  if (stride == 2) {  // forward only (H, W: the input size)
+    if (flip || addend || bnb || H % 2 || W % 2 || Cin % 64 || Nout % 64) return kNotHandled;
+    const int Ho = H / 2, Wo = W / 2;
+    D3S2FCfg c;
+    if (!pick_s2f(N, Ho, Wo, Cin, Nout, &c)) return kNotHandled;
+    const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
+    if (xbytes >= (1u << 31) || wbytes >= (1u << 31) || (size_t)N * Ho * Wo * Nout * 2 >= (1u << 31)) return kNotHandled;
+    D3Args a = {};
+    a.x = x;
+    a.w = w;
+    a.out = out;
+    a.stats = stats;
+    a.N = N;
+    a.H = Ho;
+    a.W = Wo;
+    a.iH = H;
+    a.iW = W;
+    a.Cin = Cin;
+    a.Nout = Nout;
+    a.tiles_x = Wo / c.TW;
+    a.tiles_per_img = (Ho / c.TH) * a.tiles_x;
+    a.ntm = N * a.tiles_per_img;
+    a.ntn = Nout / c.BN;
+    a.xbytes = (uint32_t)xbytes;
+    a.wbytes = (uint32_t)wbytes;
+    a.tp = probe_clock_take();
+    if (stats_rows) *stats_rows = a.ntm;
+    const dim3 grid(a.ntm * a.ntn), blk(c.threads);
+    probe_begin(st);
+    SQR_DISPATCH16(dtype, T, {
+      switch (c.id) {
+        case 0: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 32, 4, 1, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
+        case 1: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 16, 4, 2, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
+      }
+    });
+    probe_end(st);
+    SQR_HIP_LAUNCH_CHECK("conv3_kernel");
+    return 0;
+  }
   if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return kNotHandled;
   const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
   if (xbytes >= (1u << 31) || wbytes >= (1u << 31) || (size_t)N * H * W * Nout * 2 >= (1u << 31)) return kNotHandled;
@@ -1543,6 +1684,8 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   a.N = N;
   a.H = H;
   a.W = W;
+  a.iH = H;
+  a.iW = W;
   a.Cin = Cin;
   a.Nout = Nout;
   a.tiles_x = W / c.TW;

@@ -161,9 +161,10 @@ struct BnbArgs {
 };
 // addend (nullable, backward-data only): out = conv + addend, fused into the epilogue;
 // bnb (nullable, backward-data only): see BnbArgs (stats / stats_rows then receive its partials)
+// stride 2 (forward only, flip 0, no addend / bnb): H, W are the input size
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st, const void* addend = nullptr,
-                 const BnbArgs* bnb = nullptr);
+                 const BnbArgs* bnb = nullptr, int stride = 1);
 // direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,

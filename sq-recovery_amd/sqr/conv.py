@@ -176,8 +176,9 @@ def pack_all(convs, dtype):
 
 def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
     """y = conv(x); with return_ws the workspace (holding the im2col matrix for C<8) is returned
-    too; with stats the BatchNorm partials [rows, 2, K] (f32 per-tile sum / sum of squares of y,
-    see sqr_conv2d_fwd_stats) are returned after y."""
+    too; with stats the BatchNorm partials [rows, 2, K] (f32 per-tile Welford rows (mean, M2) of y,
+    their pixel counts after them in the buffer: sqr.bn.partial_counts; sqr_conv2d_fwd_stats) are
+    returned after y."""
     import ctypes
     ho, wo = _out_hw(d)
     dt = _TORCH_DT[d.dtype]

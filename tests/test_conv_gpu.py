@@ -331,6 +331,42 @@ def test_conv3s2_wgrad_vs_f64(shape, dtype):
     assert _rel(dw, dwr) <= 2e-4
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape", [(64, 64, 64, 128), (64, 128, 32, 256), (64, 256, 16, 512), (2, 64, 64, 128),
+                                   (3, 128, 32, 256), (1, 256, 16, 512), (2, 64, 128, 128), (2, 128, 64, 256),
+                                   (2, 256, 32, 512)],
+                         ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv3s2_fwd_vs_f64(shape, dtype):
+    """The direct stride-2 forward (conv3_kernel's four-plane window; layers 2-4's first conv at 256
+    and 512 input) at the bench batch and at a few images (direct forced) vs float64, and its
+    BatchNorm statistics partials vs the stored output."""
+    from sqr import conv as sc
+    from sqr._lib import lib
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(13 * N + C + K + H)
+    x = torch.randn(N, C, H, H, generator=g).to(dtype).float()
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    yr = F.conv2d(x.double(), w.to(dtype).double(), stride=2, padding=1)
+    d = sc._desc(N, C, H, H, K, 3, 3, 2, 1, dtype)
+    krsc, _ = sc.pack_weight(w.to(DEV), d, False)
+    old = lib().sqr_conv_set_direct(2)
+    try:
+        y, st = sc.conv2d_fwd(x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last), krsc, d,
+                              stats=True)
+        torch.cuda.synchronize()
+    finally:
+        lib().sqr_conv_set_direct(old)
+    assert _rel(y, yr) <= (8e-3 if dtype == torch.bfloat16 else 1e-3)
+    from sqr.bn import partial_counts
+    cnt = partial_counts(st).double()
+    assert int(cnt.sum()) == N * (H // 2) ** 2
+    yf = y.double().cpu()
+    mean = (cnt[:, None] * st[:, 0].double()).sum(0).cpu() / cnt.sum().cpu()
+    m2 = (st[:, 1].double() + cnt[:, None] * (st[:, 0].double() - mean.to(DEV)) ** 2).sum(0).cpu()
+    assert _rel(mean, yf.mean((0, 2, 3))) <= 1e-5
+    assert _rel(m2, ((yf - yf.mean((0, 2, 3), keepdim=True)) ** 2).sum((0, 2, 3))) <= 1e-5
+
+
 @pytest.mark.parametrize("shape", [(64, 128, 32, 128), (64, 256, 16, 256), (64, 512, 8, 512)],
                          ids=lambda s: "N%dC%dH%dK%d" % s)
 def test_conv3_tiled_bench_size_vs_f64(shape):
