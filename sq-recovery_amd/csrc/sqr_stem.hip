@@ -168,7 +168,9 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   V8<T> wf[4][2];
   load_wfrag<T>(w, lane, wf);
-  // per lane and channel: shifted sums of its values about its first one (sqr_common.h LaneStat)
+  // per lane and channel: sums of the values shifted by K = the channel's first value in pixel lane
+  // fr = 0 (broadcast at the first block, shared by the 16 pixel lanes of the channel, so their sums
+  // add exactly in the final xor tree; sqr_common.h LaneStat)
   LaneStat ls[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) ls[i] = LaneStat{0.f, 0.f, 0.f};
@@ -190,27 +192,33 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
       f32x4 acc[4];
       conv_block<T>((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
       // every tile pixel is a real conv output (Hc % 8 == 0, Wc % 32 == 0 checked on the host)
+      if (b == 0 && t == (int)blockIdx.x) {
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ls[jb * 4 + e].k = __shfl(rnd<T>(acc[jb][e]), lane & 48, 64);
+      }
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) lane_stat_add(ls[jb * 4 + e], rnd<T>(acc[jb][e]), t == (int)blockIdx.x && b == 0);
+        for (int e = 0; e < 4; ++e) lane_stat_add(ls[jb * 4 + e], rnd<T>(acc[jb][e]), false);
     }
   }
-  // lane (mean, M2) over its 4 * mytiles values, merged over the 16 pixel lanes by an xor tree of
-  // equal-count pairs (both partners compute the same value), then over the 4 waves in order
-  float n = (float)(4 * mytiles), m[16], q[16];
+  // the 16 pixel lanes' shifted sums add exactly (common K): xor tree, then (mean, M2) of the
+  // wave's 64 * mytiles values per channel, merged over the 4 waves in order
+  const float n = (float)(64 * mytiles);
+  float m[16], q[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) lane_stat_final(ls[i], n, &m[i], &q[i]);
+  for (int i = 0; i < 16; ++i) {
+    float sa = ls[i].s, sq = ls[i].q;
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float mb = __shfl_xor(m[i], off, 64), qb = __shfl_xor(q[i], off, 64);
-      const float d = mb - m[i];
-      m[i] = (m[i] + mb) * 0.5f;
-      q[i] = (q[i] + qb) + d * d * (n * 0.5f);
+    for (int off = 1; off < 16; off <<= 1) {
+      sa += __shfl_xor(sa, off, 64);
+      sq += __shfl_xor(sq, off, 64);
     }
-    n *= 2.f;
+    const float sn = n > 0.f ? sa / n : 0.f;
+    m[i] = ls[i].k + sn;
+    q[i] = fmaxf(sq - sa * sn, 0.f);
   }
   __syncthreads();
   if (fr == 0) {
