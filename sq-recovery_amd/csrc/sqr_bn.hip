@@ -103,13 +103,16 @@ __global__ void fwd_finalize_kernel(const P* __restrict__ part, int nblk, int M,
                                     float* __restrict__ coef) {
   const int c = fin_wave_index();
   if (c >= C) return;
+  // the channel's parameters are loaded first: their round trip overlaps the partials' (this
+  // launch is latency-bound: a chain of dependent memory round trips)
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  const float rm0 = rmean ? rmean[c] : 0.f, rv0 = rmean ? rvar[c] : 0.f;
   double mean, m2;
   merge_stats_w<P>(part, nblk, C, c, (double)M, &mean, &m2);
   if (threadIdx.x & 63) return;
   double var = m2 / M;
   var = var < 0.0 ? 0.0 : var;
   const double invstd = 1.0 / sqrt(var + (double)eps);
-  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
   const float scale = (float)(g * invstd);
   coef[c] = scale;
   coef[C + c] = (float)(bt - mean * g * invstd);
@@ -117,8 +120,8 @@ __global__ void fwd_finalize_kernel(const P* __restrict__ part, int nblk, int M,
   save_invstd[c] = (float)invstd;
   if (rmean) {
     const double unb = M > 1 ? var * M / (M - 1) : var;
-    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    rmean[c] = (float)((1.0 - momentum) * rm0 + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rv0 + momentum * unb);
   }
 }
 
@@ -274,19 +277,27 @@ struct FinJob {
   float *dgamma, *dbeta;
 };
 
-__device__ __forceinline__ void fwd_finalize_one(const FinJob& j, int c, int M, int C, double mean, double m2) {
+// a channel's forward parameters, loaded before its partials (see fwd_finalize_kernel)
+struct FinPar {
+  float g, bt, rm, rv;
+};
+__device__ __forceinline__ FinPar fin_par(const FinJob& j, int c) {
+  return FinPar{j.gamma ? j.gamma[c] : 1.f, j.beta ? j.beta[c] : 0.f, j.rmean ? j.rmean[c] : 0.f,
+                j.rmean ? j.rvar[c] : 0.f};
+}
+__device__ __forceinline__ void fwd_finalize_one(const FinJob& j, const FinPar& p, int c, int M, int C, double mean,
+                                                 double m2) {
   double var = m2 / M;
   var = var < 0.0 ? 0.0 : var;
   const double invstd = 1.0 / sqrt(var + (double)j.eps);
-  const float g = j.gamma ? j.gamma[c] : 1.f, bt = j.beta ? j.beta[c] : 0.f;
-  j.coef[c] = (float)(g * invstd);
-  j.coef[C + c] = (float)(bt - mean * g * invstd);
+  j.coef[c] = (float)(p.g * invstd);
+  j.coef[C + c] = (float)(p.bt - mean * p.g * invstd);
   j.save_mean[c] = (float)mean;
   j.save_invstd[c] = (float)invstd;
   if (j.rmean) {
     const double unb = M > 1 ? var * M / (M - 1) : var;
-    j.rmean[c] = (float)((1.0 - j.momentum) * j.rmean[c] + j.momentum * mean);
-    j.rvar[c] = (float)((1.0 - j.momentum) * j.rvar[c] + j.momentum * unb);
+    j.rmean[c] = (float)((1.0 - j.momentum) * p.rm + j.momentum * mean);
+    j.rvar[c] = (float)((1.0 - j.momentum) * p.rv + j.momentum * unb);
   }
 }
 
@@ -297,10 +308,11 @@ __global__ void fwd_finalize2_kernel(FinJob a, FinJob b, int M, int C) {
   const bool second = w >= C;
   const FinJob& j = second ? b : a;
   const int c = second ? w - C : w;
+  const FinPar fp = fin_par(j, c);
   double mean, m2;
   merge_stats_w<float>(j.part, j.nblk, C, c, (double)M, &mean, &m2);
   if (threadIdx.x & 63) return;
-  fwd_finalize_one(j, c, M, C, mean, m2);
+  fwd_finalize_one(j, fp, c, M, C, mean, m2);
 }
 
 // y = act(xa*sa + ta + xb*sb + tb)
@@ -352,6 +364,7 @@ __global__ void bwd_finalize2_kernel(const double* __restrict__ part, int nblk, 
   const bool second = w >= C;
   const FinJob& j = second ? b : a;
   const int c = second ? w - C : w;
+  const double is = j.save_invstd[c], mu = j.save_mean[c], gm = j.gamma ? j.gamma[c] : 1.0;  // before the partials
   double acc[2];
   if (second)
     sum_partials_w<double, 3, 2>(part, nblk, C, c, acc);
@@ -359,11 +372,10 @@ __global__ void bwd_finalize2_kernel(const double* __restrict__ part, int nblk, 
     sum_partials_w<double, 3, 1>(part, nblk, C, c, acc);
   if (threadIdx.x & 63) return;
   const double sg = acc[0], sgx = acc[1];
-  const double is = j.save_invstd[c], mu = j.save_mean[c];
   const double dgam = sgx * is;
   if (j.dgamma) j.dgamma[c] = (float)dgam;
   if (j.dbeta) j.dbeta[c] = (float)sg;
-  const double ak = (j.gamma ? j.gamma[c] : 1.0) * is;
+  const double ak = gm * is;
   const double k3 = -ak * is * dgam / M;
   j.coef[c] = (float)ak;
   j.coef[2 * C + c] = (float)k3;

@@ -295,15 +295,15 @@ __device__ __forceinline__ void bn_bwd_finalize_w(const P* __restrict__ part, in
                                                   const float* __restrict__ gamma, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                   float* __restrict__ dbeta, float* __restrict__ coef) {
+  const double is = invstd[c], mu = mean[c], gm = gamma ? gamma[c] : 1.0;  // before the partials: overlapped
   double acc[2];
   sum_partials_w<P>(part, nblk, C, c, acc);
   if ((threadIdx.x & 63) != 0) return;
   const double sg = acc[0], sgx = acc[1];
-  const double is = invstd[c], mu = mean[c];
   const double dgam = sgx * is;  // sum g * xhat
   if (dgamma) dgamma[c] = (float)dgam;
   if (dbeta) dbeta[c] = (float)sg;
-  const double a = (gamma ? gamma[c] : 1.0) * is;
+  const double a = gm * is;
   const double k3 = -a * is * dgam / M;
   coef[c] = (float)a;
   coef[2 * C + c] = (float)k3;
