@@ -186,6 +186,13 @@ int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx, const sqr_
  * their epilogues (the sum is never a separate pass); other shapes add after the GEMM. */
 int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void* dx, const void* addend,
                             const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
+/* The same for a stride-2 conv whose input also feeds a stride-2 1x1 downsample conv (a BasicBlock
+ * with a downsample, torch/models.py:181): that branch's input gradient is non-zero only on the
+ * (even, even) pixels, so it is passed compact, addend_c [N, H/2, W/2, C] (the downsample's
+ * backward-data as a stride-1 1x1 conv on the output grid), and added there: dx[n, 2i, 2j, c] +=
+ * addend_c[n, i, j, c].  The direct stride-2 kernel adds it in its copy-out. */
+int sqr_conv2d_bwd_data_acc_s2(const void* dy, const void* w_crsk, void* dx, const void* addend_c,
+                               const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
 /* Backward-data of a conv whose input is a BatchNorm+ReLU output — a BasicBlock's conv2 into bn1
  * (torch/models.py:181): g_out = bwd_data(dy) * relu_mask (the BatchNorm's ReLU mask, 1 bit per
  * element) and stats receives that BatchNorm's backward sums (sum g, sum g*(bn_x - bn_mean)) as

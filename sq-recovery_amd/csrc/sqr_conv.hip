@@ -1393,6 +1393,51 @@ extern "C" int sqr_conv2d_bwd_data(const void* dy, const void* w_crsk, void* dx,
   return bwd_data_impl(dy, w_crsk, dx, nullptr, d, stream);
 }
 
+// dx[n, 2i, 2j, c] += addend_c[n, i, j, c]: the fallback of sqr_conv2d_bwd_data_acc_s2
+template <typename T>
+__global__ void __launch_bounds__(256) add_s2_compact_kernel(T* __restrict__ dx, const T* __restrict__ ac, int Ho,
+                                                             int Wo, int C, long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;  // one element of addend_c
+  if (i >= n) return;
+  const long long pix = i / C;
+  const int c = (int)(i - pix * C);
+  const long long img = pix / ((long long)Ho * Wo);
+  const int rem = (int)(pix - img * Ho * Wo), y = rem / Wo, x = rem - y * Wo;
+  const size_t o = ((size_t)(img * 2 * Ho + 2 * y) * (2 * Wo) + 2 * x) * C + c;
+  dx[o] = (T)((float)dx[o] + (float)ac[i]);
+}
+
+extern "C" int sqr_conv2d_bwd_data_acc_s2(const void* dy, const void* w_crsk, void* dx, const void* addend_c,
+                                          const sqr_conv_desc* d, void* workspace, size_t workspace_bytes,
+                                          void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  Shape sh;
+  int rc = check_desc(d, &sh);
+  if (rc) return rc;
+  SQR_CHECK_ARG(dy && w_crsk && dx && addend_c, "conv2d_bwd_data_acc_s2: null pointer");
+  SQR_CHECK_ARG(d->stride == 2 && d->H == 2 * sh.Ho && d->W == 2 * sh.Wo && !sh.im2col,
+                "conv2d_bwd_data_acc_s2: needs a stride-2 conv with H = 2 Ho, W = 2 Wo");
+  hipStream_t st = as_stream(stream);
+  if (d->dtype != SQR_DTYPE_F32 && d->R == 3 && d->S == 3 && d->pad == 1) {
+    const int off[4] = {0, d->C * d->K, 3 * d->C * d->K, 5 * d->C * d->K};
+    rc = conv3s2_dgrad_launch(d->dtype, dy, w_crsk, off, dx, d->N, sh.Ho, sh.Wo, d->K, d->C, st, addend_c, 1);
+    if (rc != kNotHandled) return rc;
+  }
+  rc = bwd_data_impl(dy, w_crsk, dx, nullptr, d, stream);
+  if (rc) return rc;
+  const long long n = (long long)d->N * sh.Ho * sh.Wo * d->C;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (d->dtype == SQR_DTYPE_F32)
+    hipLaunchKernelGGL(add_s2_compact_kernel<float>, dim3(grid), dim3(256), 0, st, (float*)dx, (const float*)addend_c,
+                       sh.Ho, sh.Wo, d->C, n);
+  else
+    SQR_DISPATCH16(d->dtype, T, hipLaunchKernelGGL(add_s2_compact_kernel<T>, dim3(grid), dim3(256), 0, st, (T*)dx,
+                                                   (const T*)addend_c, sh.Ho, sh.Wo, d->C, n));
+  SQR_HIP_LAUNCH_CHECK("add_s2_compact_kernel");
+  return 0;
+}
+
 extern "C" int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void* dx, const void* addend,
                                        const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream) {
   (void)workspace;

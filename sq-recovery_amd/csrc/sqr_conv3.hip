@@ -855,6 +855,7 @@ struct D3S2Args {
   const void* w;   // parity classes back to back, class cl = [C][Rc][Sc][K]
   void* dx;        // [N][2Ho][2Wo][C]
   const void* addend;  // nullable: dx = dgrad + addend (may alias dx)
+  int addend_s2;       // 1: the addend is compact [N][Ho][Wo][C], added to the (even, even) pixels only
   int N, Ho, Wo, K, C;
   int tiles_x, tiles_per_img, ntn;
   int cls_off[4];  // elements
@@ -1034,13 +1035,24 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
     for (int u = 0; u < AG; ++u) {
       int p, sl;
       size_t go;
-      if (piece(it0 + u, ph, p, sl, go)) av[u] = *(const uint4*)((const T*)a.addend + go);
+      if (piece(it0 + u, ph, p, sl, go)) {
+        if (a.addend_s2) {  // compact addend: the (even, even) pixels of the ph = 0 half only
+          const int y = p / PX, x = p - y * PX;
+          av[u] = (x & 1) ? uint4{0u, 0u, 0u, 0u}
+                          : *(const uint4*)((const T*)a.addend +
+                                            (((size_t)img * a.Ho + i0 + y) * a.Wo + j0 + (x >> 1)) * a.C + n0 +
+                                                8 * sl);
+        } else {
+          av[u] = *(const uint4*)((const T*)a.addend + go);
+        }
+      }
     }
   };
 #pragma unroll
   for (int ph = 0; ph < 2; ++ph) {
+    const bool add = a.addend && !(a.addend_s2 && ph == 1);
     uint4 av[AG];
-    if (a.addend) load_group(0, ph, av);
+    if (add) load_group(0, ph, av);
     if (ph) __syncthreads();  // previous half copied out
 #pragma unroll
     for (int pw = 0; pw < 2; ++pw)
@@ -1058,14 +1070,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3s2_dgrad_kernel(D
     __syncthreads();
 #pragma unroll
     for (int it0 = 0; it0 < NIT; it0 += AG) {
-      if (it0 && a.addend) load_group(it0, ph, av);
+      if (it0 && add) load_group(it0, ph, av);
 #pragma unroll
       for (int u = 0; u < AG; ++u) {
         int p, sl;
         size_t go;
         if (!piece(it0 + u, ph, p, sl, go)) continue;
         uint4 v = *(const uint4*)(smem + p * (BN * 2) + ((sl ^ ((p >> 1) & 7)) << 4));
-        if (a.addend) {
+        if (add) {
           uint32_t* vv = (uint32_t*)&v;
           const uint32_t* aa = (const uint32_t*)&av[u];
 #pragma unroll
@@ -1510,7 +1522,7 @@ bool s2_pick(int Ho, int Wo, int K, int C, int* TH, int* TW, int* BN, int* nch) 
 }  // namespace
 
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,
-                         int Wo, int K, int C, hipStream_t st, const void* addend) {
+                         int Wo, int K, int C, hipStream_t st, const void* addend, int addend_s2) {
   if (g_direct == 0) return kNotHandled;
   int TH, TW, BN, nch;
   if (!s2_pick(Ho, Wo, K, C, &TH, &TW, &BN, &nch)) return kNotHandled;
@@ -1521,6 +1533,7 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
   a.w = w_cls;
   a.dx = dx;
   a.addend = addend;
+  a.addend_s2 = addend && addend_s2 ? 1 : 0;
   a.N = N;
   a.Ho = Ho;
   a.Wo = Wo;

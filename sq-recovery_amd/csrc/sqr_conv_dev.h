@@ -167,8 +167,10 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
                  const BnbArgs* bnb = nullptr, int stride = 1);
 // direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
+// addend_s2 (with addend): the addend is compact [N][Ho][Wo][C] and lands on the (even, even) dX
+// pixels only (a stride-2 1x1 downsample conv's input gradient)
 int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int* cls_off, void* dx, int N, int Ho,
-                         int Wo, int K, int C, hipStream_t st, const void* addend = nullptr);
+                         int Wo, int K, int C, hipStream_t st, const void* addend = nullptr, int addend_s2 = 0);
 // direct 3x3 / pad-1 / stride 1 or 2 bf16 weight gradient: fp32 slabs [splits][K][C][3][3] (torch's
 // KCRS order: the gradient is their elementwise sum, wgrad_sum_kernel).  conv3w_slab_bytes = 0 if
 // not handled.  H, W: the input's size.

@@ -8,6 +8,8 @@ torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
 Compute dtype: bfloat16 / float16 when the input has that dtype or CUDA autocast is on with it,
 else float32 (exact-f32 MFMA: the parity mode).
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -256,6 +258,40 @@ def conv2d_bwd_data_acc(gy, w_crsk, d, addend):
     return dx
 
 
+def conv2d_bwd_data_acc_s2(gy, w_crsk, d, addend_c):
+    """bwd_data(gy) of a stride-2 conv + a compact [N, C, H/2, W/2] addend on the (even, even)
+    pixels (sqr_conv2d_bwd_data_acc_s2: a stride-2 1x1 downsample branch's input gradient)."""
+    import ctypes
+    dt = _TORCH_DT[d.dtype]
+    dx = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=gy.device, memory_format=_CL)
+    ws, n = _ws(d, 1, gy.device)
+    with _Probe("dgrad", d):
+        rc = lib().sqr_conv2d_bwd_data_acc_s2(ptr(gy), ptr(w_crsk), ptr(dx), ptr(addend_c), ctypes.byref(d), ptr(ws),
+                                              n, stream_ptr(gy.device))
+    check(rc, "sqr_conv2d_bwd_data_acc_s2")
+    return dx
+
+
+# SQR_COMPACT_S2=0 keeps the full-size downsample input gradient (same-box A/B switch)
+_COMPACT_S2 = os.environ.get("SQR_COMPACT_S2", "1") != "0"
+
+
+class CompactS2:
+    """The input gradient of a stride-2 1x1 (pad 0) downsample conv kept compact: t [N, C, H/2, W/2]
+    holds the (even, even) pixels, the rest is zero.  Deposited in a ResidualJoin, it is added by
+    conv1's stride-2 backward-data copy-out (sqr_conv2d_bwd_data_acc_s2) instead of being written
+    as a full, three-quarters-zero tensor and read back."""
+    __slots__ = ("t", "shape")
+
+    def __init__(self, t, shape):
+        self.t, self.shape = t, tuple(shape)
+
+    def full(self):
+        out = torch.zeros(self.shape, dtype=self.t.dtype, device=self.t.device, memory_format=_CL)
+        out[:, :, ::2, ::2] = self.t
+        return out
+
+
 def conv2d_bwd_data_bn(gy, w_crsk, d, bn_x, bn_mask, bn_mean):
     """(g, partials): g = bwd_data(gy) * bn_mask and the following BatchNorm's backward sums
     [rows, 2, C] (sqr_conv2d_bwd_data_bn: the direct kernels compute both in their epilogues)."""
@@ -488,21 +524,39 @@ class Conv2dFn(torch.autograd.Function):
             if crsk is None:
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
             addend = ctx.join.take() if (ctx.join is not None and ctx.role == "acc") else None
+            s2 = isinstance(addend, CompactS2)
+            if s2 and not (d.stride == 2 and addend.t.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W)
+                           and tuple(addend.t.shape) == (d.N, d.C, d.H // 2, d.W // 2) and d.H % 2 == 0
+                           and d.W % 2 == 0 and addend.t.is_contiguous(memory_format=_CL)):
+                addend, s2 = addend.full(), False
             link = ctx.bnb if (ctx.bnb is not None and ctx.bnb.ready() and addend is None) else None
             if link is not None and link.x.dtype == dt:
                 dx, link.stats = conv2d_bwd_data_bn(g, crsk, d, link.x, link.mask, link.mean)
                 link.g = dx
+            elif s2:
+                dx = conv2d_bwd_data_acc_s2(g, crsk, d, addend.t)
+                ride_red = ctx.bnr  # dx is the whole gradient of x: its BatchNorm reduction can ride
             elif addend is not None and addend.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W) \
                     and addend.is_contiguous(memory_format=_CL):
                 dx = conv2d_bwd_data_acc(g, crsk, d, addend)
                 ride_red = ctx.bnr  # dx is the whole gradient of x: its BatchNorm reduction can ride
+            elif _COMPACT_S2 and ctx.join is not None and ctx.role == "dep" and not ctx.join.acc_done and d.R == 1 and d.S == 1 \
+                    and d.stride == 2 and d.pad == 0 and d.H % 2 == 0 and d.W % 2 == 0 and d.C >= 8:
+                # stride-2 1x1 downsample: only the (even, even) pixels of its input gradient are
+                # non-zero — computed as a stride-1 1x1 backward-data on the output grid and
+                # deposited compact for conv1's stride-2 backward-data (CompactS2)
+                d1 = _desc(d.N, d.C, d.H // 2, d.W // 2, d.K, 1, 1, 1, 0, dt)
+                dx = CompactS2(conv2d_bwd_data(g, crsk, d1).to(ctx.x_dtype), (d.N, d.C, d.H, d.W))
             else:
                 dx = conv2d_bwd_data(g, crsk, d)
                 if addend is not None:
                     dx = dx + addend
-            dx = dx.to(ctx.x_dtype)
+            if not isinstance(dx, CompactS2):
+                dx = dx.to(ctx.x_dtype)
             if ctx.join is not None and ctx.role == "dep":
                 dx = ctx.join.deposit(dx)
+                if isinstance(dx, CompactS2):  # (not deposited: conv1's backward already ran)
+                    dx = dx.full()
         if ctx.needs_input_grad[1]:
             fin = None
             link = ctx.bnb

@@ -485,6 +485,37 @@ def test_conv_bwd_data_acc(shape, dtype):
 # sqr_conv2d_bwd_data_bn (a BasicBlock's conv2 backward-data feeding bn1's backward): g = dgrad * mask
 # and the per-channel sums (sum g, sum g*(x - mean)) — the persistent layer-1 kernel (ring wrap at
 # the bench batch), the tiled kernels of layers 2-4, and the implicit-GEMM fallback (fp32, odd size).
+# sqr_conv2d_bwd_data_acc_s2: a stride-2 conv's dgrad + a compact [N, C, H/2, W/2] addend on the
+# (even, even) pixels (the stride-2 1x1 downsample branch of a BasicBlock's input gradient): the direct
+# stride-2 kernel's copy-out (layers 2-4, 256 and 512 input) and the implicit GEMM + scatter-add fallback
+# (fp32, and a 1x1 conv)
+S2C_SHAPES = [(4, 64, 64, 128, 3), (64, 64, 64, 128, 3), (4, 128, 32, 256, 3), (64, 256, 16, 512, 3),
+              (16, 128, 64, 256, 3), (2, 64, 128, 128, 3), (4, 64, 64, 128, 1)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=["bf16", "f16", "f32"])
+@pytest.mark.parametrize("shape", S2C_SHAPES, ids=lambda s: "N%dC%dH%dK%dR%d" % s)
+def test_conv_bwd_data_acc_s2(shape, dtype):
+    from sqr import conv as sc
+    N, C, H, K, R = shape
+    if dtype == torch.float32 and N > 8:
+        pytest.skip("fp32 runs the implicit GEMM + scatter-add; the small batch covers it")
+    pad = R // 2
+    g = torch.Generator().manual_seed(17 * N + C + K + R)
+    w = torch.randn(K, C, R, R, generator=g) / (C * R * R) ** 0.5
+    gy = torch.randn(N, K, H // 2, H // 2, generator=g).to(dtype).float()
+    addc = torch.randn(N, C, H // 2, H // 2, generator=g).to(dtype).float()
+    d = sc._desc(N, C, H, H, K, R, R, 2, pad, dtype)
+    _, crsk = sc.pack_weight(w.to(DEV), d, True)
+    cl = dict(memory_format=torch.channels_last)
+    dx = sc.conv2d_bwd_data_acc_s2(gy.to(DEV).to(dtype).contiguous(**cl), crsk, d,
+                                   addc.to(DEV).to(dtype).contiguous(**cl))
+    torch.cuda.synchronize()
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.to(dtype).double(), gy.double(), stride=2, padding=pad)
+    ref[:, :, ::2, ::2] += addc.double()
+    assert _rel(dx, ref) <= {torch.bfloat16: 1.2e-2, torch.float16: 2e-3, torch.float32: 1e-5}[dtype]
+
+
 BNB_SHAPES = [(4, 64, 64, 64), (64, 64, 64, 64), (4, 128, 32, 128), (64, 128, 32, 128), (4, 256, 16, 256),
               (4, 512, 8, 512), (2, 64, 128, 64), (3, 32, 20, 32), (16, 128, 64, 128), (16, 256, 32, 256)]
 
