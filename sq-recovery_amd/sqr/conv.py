@@ -8,8 +8,6 @@ torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
 Compute dtype: bfloat16 / float16 when the input has that dtype or CUDA autocast is on with it,
 else float32 (exact-f32 MFMA: the parity mode).
 """
-import os
-
 import torch
 import torch.nn as nn
 
@@ -270,10 +268,6 @@ def conv2d_bwd_data_acc_s2(gy, w_crsk, d, addend_c):
                                               n, stream_ptr(gy.device))
     check(rc, "sqr_conv2d_bwd_data_acc_s2")
     return dx
-
-
-# SQR_COMPACT_S2=0 keeps the full-size downsample input gradient (same-box A/B switch)
-_COMPACT_S2 = os.environ.get("SQR_COMPACT_S2", "1") != "0"
 
 
 class CompactS2:
@@ -540,7 +534,7 @@ class Conv2dFn(torch.autograd.Function):
                     and addend.is_contiguous(memory_format=_CL):
                 dx = conv2d_bwd_data_acc(g, crsk, d, addend)
                 ride_red = ctx.bnr  # dx is the whole gradient of x: its BatchNorm reduction can ride
-            elif _COMPACT_S2 and ctx.join is not None and ctx.role == "dep" and not ctx.join.acc_done and d.R == 1 and d.S == 1 \
+            elif ctx.join is not None and ctx.role == "dep" and not ctx.join.acc_done and d.R == 1 and d.S == 1 \
                     and d.stride == 2 and d.pad == 0 and d.H % 2 == 0 and d.W % 2 == 0 and d.C >= 8:
                 # stride-2 1x1 downsample: only the (even, even) pixels of its input gradient are
                 # non-zero — computed as a stride-1 1x1 backward-data on the output grid and
