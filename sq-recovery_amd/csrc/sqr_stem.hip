@@ -128,36 +128,50 @@ __device__ __forceinline__ void conv_block(const char* win, int woff, int lane, 
 }
 
 // Input window rows [y0, y0 + WR) x cols [x0, x0 + WC) staged through registers: load() issues
-// the (branch-free, clamped) global loads of a tile early, store() writes them as bf16 into the LDS
-// window (pitch WPITCH) — the persistent loops prefetch tile t+1 while tile t computes.
-template <typename TI, typename T, int WR, int WC>
+// the (branch-free, clamped) global loads of a tile early, store() writes them as T into the LDS
+// window (pitch WPITCH) — the persistent loops prefetch ahead while a tile computes.  Every tile's
+// x0 is SH (mod 4), so a row is read as aligned 4-element vectors from x0 - SH (W % 4 == 0: a
+// vector is wholly inside or wholly outside the image) and shifted by SH elements on the LDS store.
+template <typename TI, typename T, int WR, int WC, int SH>
 struct Window {
-  static constexpr int NE = WR * WC, KW = (NE + 255) / 256;
-  float v[KW];
+  static constexpr int QPR = (WC + SH + 3) / 4;  // 4-element vectors per row
+  static constexpr int NQ = WR * QPR, KW = (NQ + 255) / 256;
+  typedef TI V4 __attribute__((ext_vector_type(4)));
+  V4 v[KW];
   __device__ __forceinline__ void load(const TI* __restrict__ img, int H, int W, int y0, int x0) {
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
       const int i = threadIdx.x + 256 * k;
-      const int r = i / WC, c = i - r * WC;
-      const int y = y0 + r, x = x0 + c;
-      const bool ok = i < NE && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-      const int yc = min(max(y, 0), H - 1), xc = min(max(x, 0), W - 1);
-      const float t = (float)img[(size_t)yc * W + xc];
-      v[k] = ok ? t : 0.f;
+      const int r = i / QPR, m = i - r * QPR;
+      const int y = y0 + r, x = x0 - SH + 4 * m;
+      const bool ok = i < NQ && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const V4 t = *(const V4*)(img + (ok ? (size_t)y * W + x : 0));
+      v[k] = ok ? t : V4{};
     }
   }
   __device__ __forceinline__ void store(uint16_t* win) const {
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
       const int i = threadIdx.x + 256 * k;
-      const int r = i / WC, c = i - r * WC;
-      if (i < NE) win[r * WPITCH + c] = hbits<T>(v[k]);
+      const int r = i / QPR, m = i - r * QPR;
+      if (i < NQ) {
+        const uint32_t p[2] = {pk16<T>((float)v[k][0], (float)v[k][1]), pk16<T>((float)v[k][2], (float)v[k][3])};
+        uint16_t* row = win + r * WPITCH;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * m + e - SH;
+          if (c >= 0 && c < WC) row[c] = (uint16_t)(p[e >> 1] >> (16 * (e & 1)));
+        }
+      }
     }
   }
 };
 
 // ---------------------------------------------------------------- S1: BN statistics
-// tile = 8 conv rows x 32 conv cols (16 MFMA pixel blocks, 4 per wave); window 22 x 70
+// tile = 8 conv rows x 32 conv cols (16 MFMA pixel blocks, 4 per wave); window 22 x 70.  The input
+// windows are prefetched two tiles ahead (two register sets, alternating), and the statistics run
+// on channel pairs in packed fp32 (v_pk_add / v_pk_fma: 1.5 instructions per value after the RNE
+// rounding to T).
 template <typename TI, typename T>
 __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ img, const float* __restrict__ w,
                                                          int H, int W, int tiles_x, int tiles_img, int ntiles,
@@ -168,41 +182,53 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   V8<T> wf[4][2];
   load_wfrag<T>(w, lane, wf);
-  // per lane and channel: sums of the values shifted by K = the channel's first value in pixel lane
-  // fr = 0 (broadcast at the first block, shared by the 16 pixel lanes of the channel, so their sums
-  // add exactly in the final xor tree; sqr_common.h LaneStat)
-  LaneStat ls[16];
+  // per lane and channel pair i (channels 16 (i / 2) + 4 fq + 2 (i % 2) + {0, 1}): sums of the values
+  // shifted by K = the channel's first value in pixel lane fr = 0 (broadcast at the first block,
+  // shared by the 16 pixel lanes of the channel, so their sums add exactly in the final xor tree;
+  // sqr_common.h LaneStat)
+  f32x2 K2[8], S2[8], Q2[8];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) ls[i] = LaneStat{0.f, 0.f, 0.f};
-  Window<TI, T, 22, 70> pf;
-  auto fetch = [&](int t) {
+  for (int i = 0; i < 8; ++i) K2[i] = S2[i] = Q2[i] = f32x2{0.f, 0.f};
+  Window<TI, T, 22, 70, 1> pfa, pfb;
+  auto fetch = [&](Window<TI, T, 22, 70, 1>& pf, int t) {
     const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
     pf.load(img + (size_t)n * H * W, H, W, 16 * ty - 3, 64 * tx - 3);
   };
-  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x);
-  int mytiles = 0;
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x, ++mytiles) {
+  const int G = gridDim.x;
+  int t = blockIdx.x, mytiles = 0;
+  if (t < ntiles) fetch(pfa, t);
+  if (t + G < ntiles) fetch(pfb, t + G);
+  auto tile = [&](Window<TI, T, 22, 70, 1>& pf) {
     __syncthreads();  // previous tile's window reads are done
     pf.store(win);
     __syncthreads();
-    if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);  // next tile's loads fly during this one's MFMAs
+    if (t + 2 * G < ntiles) fetch(pf, t + 2 * G);  // two tiles ahead: the loads fly for two tiles' MFMAs
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int q = (wave * 4 + b) * 16 + fr, py = q >> 5, px = q & 31;
       f32x4 acc[4];
       conv_block<T>((const char*)win, 2 * py * WPITCH * 2 + 4 * px, lane, wf, acc);
       // every tile pixel is a real conv output (Hc % 8 == 0, Wc % 32 == 0 checked on the host)
-      if (b == 0 && t == (int)blockIdx.x) {
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ls[jb * 4 + e].k = __shfl(rnd<T>(acc[jb][e]), lane & 48, 64);
-      }
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) lane_stat_add(ls[jb * 4 + e], rnd<T>(acc[jb][e]), false);
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t xb = pk16<T>(acc[jb][2 * h], acc[jb][2 * h + 1]);  // the T conv output
+          const f32x2 v = {plo<T>(xb), phi<T>(xb)};
+          const int i = 2 * jb + h;
+          if (b == 0 && mytiles == 0) K2[i] = f32x2{__shfl(v[0], lane & 48, 64), __shfl(v[1], lane & 48, 64)};
+          const f32x2 d = v - K2[i];
+          S2[i] += d;
+          Q2[i] = __builtin_elementwise_fma(d, d, Q2[i]);
+        }
     }
+    t += G;
+    ++mytiles;
+  };
+  while (t < ntiles) {
+    tile(pfa);
+    if (t >= ntiles) break;
+    tile(pfb);
   }
   // the 16 pixel lanes' shifted sums add exactly (common K): xor tree, then (mean, M2) of the
   // wave's 64 * mytiles values per channel, merged over the 4 waves in order
@@ -210,14 +236,14 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
   float m[16], q[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    float sa = ls[i].s, sq = ls[i].q;
+    float sa = S2[i >> 1][i & 1], sq = Q2[i >> 1][i & 1];
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) {
       sa += __shfl_xor(sa, off, 64);
       sq += __shfl_xor(sq, off, 64);
     }
     const float sn = n > 0.f ? sa / n : 0.f;
-    m[i] = ls[i].k + sn;
+    m[i] = K2[i >> 1][i & 1] + sn;
     q[i] = fmaxf(sq - sa * sn, 0.f);
   }
   __syncthreads();
@@ -272,7 +298,7 @@ __global__ void __launch_bounds__(256) stem_pool_kernel(const TI* __restrict__ i
       sc[jb * 4 + e] = coef[16 * jb + 4 * fq + e];
       sh[jb * 4 + e] = coef[KC + 16 * jb + 4 * fq + e];
     }
-  Window<TI, T, S2_WR, S2_WC> pf;
+  Window<TI, T, S2_WR, S2_WC, 3> pf;
   auto fetch = [&](int t) {
     const int n = t / ptiles_img, rem = t - n * ptiles_img, pty = rem / ptx, ptxx = rem - pty * ptx;
     pf.load(img + (size_t)n * H * W, H, W, 2 * (2 * pty * PTH - 1) - 3, 2 * (2 * ptxx * PTW - 1) - 3);
@@ -423,7 +449,7 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
   const int oct = tid & 15;  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
 
   // register prefetch of the next tile's input window and pooled-gradient inputs
-  Window<TI, T, 14, 70> pw;
+  Window<TI, T, 14, 70, 1> pw;
   PoolIn pin;
   auto fetch = [&](int t) {
     const int n = t / tiles_img, rem = t - n * tiles_img, ty = rem / tiles_x, tx = rem - ty * tiles_x;
@@ -618,6 +644,7 @@ int stem_geom(int N, int H, int W, StemGeom* g) {
   g->Wp = (g->Wc + 2 - 3) / 2 + 1;
   SQR_CHECK_ARG(g->Hc % 8 == 0 && g->Wc % 32 == 0 && g->Hp % PTH == 0 && g->Wp % PTW == 0,
                 "stem_fused: conv1 output %dx%d must tile by 8x32 (pooled by 4x16)", g->Hc, g->Wc);
+  SQR_CHECK_ARG(W % 4 == 0, "stem_fused: input width %d must be a multiple of 4 (vector window rows)", W);
   SQR_CHECK_ARG((long long)N * g->Hp * g->Wp * KC < (1ll << 31), "stem_fused: output too large");
   return 0;
 }
@@ -680,6 +707,7 @@ extern "C" int sqr_stem_fused_fwd(const void* x, int x_dtype, int y_dtype, int N
   int rc = stem_geom(N, H, W, &g);
   if (rc) return rc;
   SQR_CHECK_ARG(x && w && y && workspace, "stem_fused_fwd: null pointer");
+  SQR_CHECK_ARG(((uintptr_t)x & (x_dtype == SQR_DTYPE_F32 ? 15 : 7)) == 0, "stem_fused_fwd: x not 4-element aligned");
   SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16 || x_dtype == SQR_DTYPE_F16,
                 "stem_fused_fwd: bad x dtype");
   SQR_CHECK_ARG(y_dtype == SQR_DTYPE_BF16 || y_dtype == SQR_DTYPE_F16, "stem_fused_fwd: bad y dtype");
@@ -718,6 +746,7 @@ extern "C" int sqr_stem_fused_bwd(const void* x, int x_dtype, int y_dtype, int N
   if (rc) return rc;
   SQR_CHECK_ARG(x && w && save_mean && save_invstd && dy && y && argmax && dw && workspace,
                 "stem_fused_bwd: null pointer");
+  SQR_CHECK_ARG(((uintptr_t)x & (x_dtype == SQR_DTYPE_F32 ? 15 : 7)) == 0, "stem_fused_bwd: x not 4-element aligned");
   SQR_CHECK_ARG(x_dtype == SQR_DTYPE_F32 || x_dtype == SQR_DTYPE_BF16 || x_dtype == SQR_DTYPE_F16,
                 "stem_fused_bwd: bad x dtype");
   SQR_CHECK_ARG(y_dtype == SQR_DTYPE_BF16 || y_dtype == SQR_DTYPE_F16, "stem_fused_bwd: bad y dtype");

@@ -430,6 +430,8 @@ def fused_stem_ok(x, conv, bn):
         return False
     if bn.num_features != 64 or not bn.affine:
         return False
+    if x.data_ptr() % (4 * x.element_size()) != 0:  # the kernels read 4-pixel row vectors
+        return False
     return bool(lib().sqr_stem_fused_supported(x.shape[0], x.shape[2], x.shape[3]))
 
 

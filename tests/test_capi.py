@@ -35,3 +35,8 @@ def test_argument_validation_without_gpu():
     assert rc == -1
     assert b"B=0" in L.sqr_last_error_string()
     assert L.sqr_implicit_loss_workspace_bytes(4, 32) == 4 * 4 * 18 * 4
+    # fused stem geometry: conv1 output tiles by 8 x 32 and the input rows are read as 4-pixel vectors
+    assert L.sqr_stem_fused_supported(2, 256, 256) == 1
+    assert L.sqr_stem_fused_supported(2, 512, 512) == 1
+    assert L.sqr_stem_fused_supported(2, 64, 63) == 0  # conv1 width 32, but W % 4 != 0
+    assert L.sqr_stem_fused_supported(2, 64, 96) == 0  # conv1 width 48
