@@ -29,6 +29,15 @@ namespace conv {
 // 16-B slot XOR key of a 128-B LDS row (see the header): shift-invariant conflict-free b128 reads
 __device__ __forceinline__ int d3key(int row) { return row & 6; }
 
+// Window key of 8-pixel-wide tiles (TW = 8, window rows WWID = 10 pixels): a fragment's 16 pixels
+// are two runs of 8 window rows, 10 apart, which row & 6 serves 2-way conflicted (the runs' rows
+// share parity and key).  Key of row r = entry r % 20 of a 20-entry table (3 bits each), found by
+// search over every fragment read the kernel makes (tap offsets r*10 + c, pixel rows y even, both
+// images of a two-image tile, flipped taps): every ds_read_b128 lane group hits 16 distinct bank
+// quads.
+constexpr unsigned long long K20_LUT = 0xadc1f8859b07e93ull;
+__device__ __forceinline__ int k20key(int row) { return (int)((K20_LUT >> (3 * (row % 20))) & 7); }
+
 struct D3Args {
   const void* x;    // [N][H][W][Cin]
   const void* w;    // [Nout][9][Cin]
@@ -171,6 +180,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   constexpr int TM = WM / 16, TN = WN / 16;
   static_assert(S == 1 || (S == 2 && IMGS == 1 && !ACC && !BNB), "stride 2: forward, one image per tile");
   constexpr int WWID = S == 1 ? TW + 2 : TW + 1;
+  constexpr bool K20 = S == 1 && TW == 8;  // window rows keyed by k20key (8-pixel-wide tiles)
   constexpr int P0 = (TH + 1) * WWID, P1 = TH * WWID;  // stride 2: rows of an a = 0 / a = 1 plane
   constexpr int WRI = S == 1 ? (TH + 2) * WWID : 2 * P0 + 2 * P1, WR = IMGS * WRI;  // halo window rows
   constexpr int WROWS = (WR + 8 * NW - 1) / (8 * NW) * (8 * NW);
@@ -231,7 +241,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int i = 0; i < WP; ++i) {
     const int r = (i * NW + wave) * 8 + prow;  // window row
-    const int ls = pslot ^ d3key(r);      // logical 16-B channel slot this lane fetches
+    const int ls = pslot ^ (K20 ? k20key(r) : d3key(r));  // logical 16-B channel slot this lane fetches
     const int ii = r / WRI, rr = r - ii * WRI;     // image of the tile, row in its window
     int h, w;
     bool used = r < WR;
@@ -263,11 +273,20 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 
   // ---- fragment coordinates
   int qbase[TM];  // window row of this lane's output pixel at tap shift (0, 0)
+  // K20: the window keys of row qbase + toff for the 6 tap offsets mod 20 (c + 10 b, b < 2, c < 3),
+  // 3 bits each
+  int qkey[K20 ? TM : 1];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wm * WM + 16 * i + fr;
     const int ii = m / (TH * TW), mm = m - ii * (TH * TW);
     qbase[i] = ii * WRI + (mm / TW) * WWID + (mm % TW);
+    if constexpr (K20) {
+      int kk = 0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) kk |= k20key(qbase[i] + (j % 3) + 10 * (j / 3)) << (3 * j);
+      qkey[i] = kk;
+    }
   }
   int poff[TN];
 #pragma unroll
@@ -340,12 +359,15 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       }
       const char* bst = bring + (PD == 2 ? (t % 3) : (step % STAGES)) * TILE_B;
       int qoff[TM];
+      // K20: tap offset toff = 10 r' + c' (r', c' the possibly flipped tap) is 10 (r' & 1) + c' mod 20
+      const int kj = K20 ? 3 * ((flip ? 2 - c3 : c3) + 3 * ((flip ? 2 - r : r) & 1)) : 0;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         int row = qbase[i] + toff;
         // keep the per-tap address math here: hoisted for all 9 unrolled taps it spills
         asm volatile("" : "+v"(row));
-        qoff[i] = row * ROWB + ((fq ^ d3key(row)) << 4);
+        const int key = K20 ? (qkey[i] >> kj) & 7 : d3key(row);
+        qoff[i] = row * ROWB + ((fq ^ key) << 4);
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
