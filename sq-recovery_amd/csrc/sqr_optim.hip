@@ -27,6 +27,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int MAXJ = 40;      // jobs per launch (kernel-argument table)
 constexpr int CHUNK = 2048;   // elements per workgroup of a plain (non-conv) parameter
+constexpr int ROWU = 5;       // float4 groups per thread of a conv-weight row held in registers (C*R*S <= 5120)
 
 struct Job {
   float *p, *m, *v;
@@ -118,7 +119,43 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   // conv weight: row k = local, CRS = C * RS contiguous elements w[k][c][tap]
   const int k = local, CRS = jb.C * jb.RS;
   const size_t base = (size_t)k * CRS;
-  if (jb.vec) {
+  if (jb.vec && CRS <= 4 * 256 * ROWU) {
+    // the whole row in one round trip: every load of the thread is issued before the first update
+    // (upd4's loads and stores alias as far as the compiler knows, so a loop of upd4 calls would
+    // serialise a memory round trip per float4 group)
+    const int n4 = CRS >> 2;
+    const size_t b4 = base >> 2;
+    f32x4 P[ROWU], M[ROWU], V[ROWU], G[ROWU];
+#pragma unroll
+    for (int u = 0; u < ROWU; ++u) {
+      const int q = threadIdx.x + 256 * u;
+      if (q < n4) {
+        P[u] = ((const f32x4*)jb.p)[b4 + q];
+        M[u] = ((const f32x4*)jb.m)[b4 + q];
+        V[u] = ((const f32x4*)jb.v)[b4 + q];
+        G[u] = ((const f32x4*)jb.g)[b4 + q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < ROWU; ++u) {
+      const int q = threadIdx.x + 256 * u;
+      if (q < n4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float pe = P[u][e], me = M[u][e], ve = V[u][e];
+          adam_update(pe, me, ve, gsc == 1.f ? G[u][e] : G[u][e] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s,
+                      J.eps);
+          P[u][e] = pe;
+          M[u][e] = me;
+          V[u][e] = ve;
+        }
+        ((f32x4*)jb.p)[b4 + q] = P[u];
+        ((f32x4*)jb.m)[b4 + q] = M[u];
+        ((f32x4*)jb.v)[b4 + q] = V[u];
+        *(f32x4*)(lds + 4 * q) = P[u];
+      }
+    }
+  } else if (jb.vec) {
     const int n4 = CRS >> 2;
     for (int q = threadIdx.x; q < n4; q += 512) {
       upd4((base >> 2) + q, lds + 4 * q);
