@@ -405,7 +405,7 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config (module doc)")
     ap.add_argument("--render", type=int, default=0, help="ImplicitLoss render size R (0 = the config's)")
     ap.add_argument("--dtype", default="", choices=("", "bf16", "fp16"), help="compute dtype (default: the config's)")
-    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU-baseline steps (0 = skip)")
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU-baseline steps (0 = skip; 5 ≈ 11 s at 16 threads)")
     ap.add_argument("--cpu1-steps", type=int, default=5, help="timed config-1 CPU steps (0 = skip)")
     ap.add_argument("--profile", action="store_true",
                     help="rocprof mode: nothing runs after the timed region (no probe / loss timing / CPU "
