@@ -193,6 +193,15 @@ int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void* dx, const 
  * addend_c[n, i, j, c].  The direct stride-2 kernel adds it in its copy-out. */
 int sqr_conv2d_bwd_data_acc_s2(const void* dy, const void* w_crsk, void* dx, const void* addend_c,
                                const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
+/* As sqr_conv2d_bwd_data_acc with the addend ReLU-masked on the fly: dx = bwd_data(dy) + addend *
+ * [bit of addend_mask] (1 bit per element, NHWC order, bit k of byte i = element 8i + k): an identity
+ * block's residual gradient g = dy_out * [y_out > 0] read as (dy_out, mask) instead of a
+ * materialised copy (torchvision BasicBlock `out += identity; relu(out)`, models.py:181).  Direct
+ * 3x3 / stride-1 16-bit kernels only: SQR_E_UNSUPPORTED otherwise (the caller masks and calls
+ * sqr_conv2d_bwd_data_acc). */
+int sqr_conv2d_bwd_data_acc_masked(const void* dy, const void* w_crsk, void* dx, const void* addend,
+                                   const uint8_t* addend_mask, const sqr_conv_desc* d, void* workspace,
+                                   size_t workspace_bytes, void* stream);
 /* Backward-data of a conv whose input is a BatchNorm+ReLU output — a BasicBlock's conv2 into bn1
  * (torch/models.py:181): g_out = bwd_data(dy) * relu_mask (the BatchNorm's ReLU mask, 1 bit per
  * element) and stats receives that BatchNorm's backward sums (sum g, sum g*(bn_x - bn_mean)) as

@@ -1446,6 +1446,27 @@ extern "C" int sqr_conv2d_bwd_data_acc(const void* dy, const void* w_crsk, void*
   return bwd_data_impl(dy, w_crsk, dx, addend, d, stream);
 }
 
+extern "C" int sqr_conv2d_bwd_data_acc_masked(const void* dy, const void* w_crsk, void* dx, const void* addend,
+                                              const uint8_t* addend_mask, const sqr_conv_desc* d, void* workspace,
+                                              size_t workspace_bytes, void* stream) {
+  (void)workspace;
+  (void)workspace_bytes;
+  Shape sh;
+  int rc = check_desc(d, &sh);
+  if (rc) return rc;
+  SQR_CHECK_ARG(dy && w_crsk && dx && addend && addend_mask, "conv2d_bwd_data_acc_masked: null pointer");
+  SQR_CHECK_ARG(addend != dx, "conv2d_bwd_data_acc_masked: addend must not alias dx");
+  rc = kNotHandled;
+  if (!sh.im2col && direct3(d, sh))
+    rc = conv3_launch(d->dtype, dy, w_crsk, dx, d->N, d->H, d->W, d->K, d->C, 1, nullptr, nullptr, as_stream(stream),
+                      addend, nullptr, 1, addend_mask);
+  if (rc == kNotHandled) {
+    set_error("conv2d_bwd_data_acc_masked: only the direct 3x3 / stride-1 16-bit kernels take a masked addend");
+    return SQR_E_UNSUPPORTED;
+  }
+  return rc;
+}
+
 extern "C" size_t sqr_conv2d_bwd_data_bn_stats_floats(const sqr_conv_desc* d) {
   Shape sh;
   if (check_desc(d, &sh)) return 0;

@@ -43,6 +43,7 @@ struct D3Args {
   const void* w;    // [Nout][9][Cin]
   void* out;        // [N][H][W][Nout]
   const void* addend;  // nullable: out = conv + addend ([N][H][W][Nout], may alias out)
+  const uint8_t* addend_mask;  // nullable (ACC): the addend counts only where its bit is set (1 bit / element)
   const void* bn_x;        // BNB: the following BatchNorm's input [N][H][W][Nout], its ReLU mask and
   const uint8_t* bn_mask;  //      batch mean: out = conv * mask, stats = (sum g, sum g*(x - mean))
   const float* bn_mean;
@@ -213,7 +214,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     return (((size_t)(img + ii) * a.H + h0 + mm / TW) * a.W + w0 + (mm % TW)) * a.Nout + n0 + wn * WN + 4 * fq;
   };
   u32x2 av[ACC || BNB ? TN : 1][ACC || BNB ? TM : 1];
-  uint32_t bmk[BNB ? TN : 1][BNB ? TM : 1];
+  uint32_t bmk[(BNB || ACC) ? TN : 1][(BNB || ACC) ? TM : 1];
   // LATE: 4-wave workgroups with 64 x 64 wave tiles (TM * TN >= 16) load the addend / BatchNorm
   // operands in the epilogue instead of holding them through the main loop: held, they take the
   // kernel past 256 VGPRs and halve its occupancy from two workgroups per CU to one (config 5's
@@ -229,6 +230,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       for (int j = 0; j < TN; ++j) {
         av[j][i] = *(const u32x2*)(ad + o + 16 * j);
         if constexpr (BNB) bmk[j][i] = a.bn_mask[(o + 16 * j) >> 3];
+        if constexpr (ACC) bmk[j][i] = a.addend_mask ? a.addend_mask[(o + 16 * j) >> 3] : 0xffu;
       }
     }
   };
@@ -420,15 +422,18 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
   for (int i = 0; i < TM; ++i) opix[i] = out_off(i);
   if constexpr ((ACC || BNB) && LATE) load_av();
-  if constexpr (ACC) {
+  if constexpr (ACC) {  // (a masked addend: cleared halves are +0, as the masked tensor would hold)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        acc[j][i][0] += lo2f<T>(av[j][i][0]);
-        acc[j][i][1] += hi2f<T>(av[j][i][0]);
-        acc[j][i][2] += lo2f<T>(av[j][i][1]);
-        acc[j][i][3] += hi2f<T>(av[j][i][1]);
+        const uint32_t mb = (bmk[j][i] >> ((opix[i] + 16 * j) & 4)) & 0xfu;
+        const uint32_t a0 = av[j][i][0] & (((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u));
+        const uint32_t a1 = av[j][i][1] & (((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u));
+        acc[j][i][0] += lo2f<T>(a0);
+        acc[j][i][1] += hi2f<T>(a0);
+        acc[j][i][2] += lo2f<T>(a1);
+        acc[j][i][3] += hi2f<T>(a1);
       }
   }
   uint32_t pk[TN][TM][2];
@@ -499,6 +504,7 @@ struct D3PArgs {
   const void* w;   // [64][9][64]
   void* out;       // [N][H][64][64]
   const void* addend;  // ACC launches: out = conv + addend (backward-data of a block input; may alias out)
+  const uint8_t* addend_mask;  // nullable (ACC): the addend counts only where its bit is set
   const void* bn_x;        // BNB launches: the following BatchNorm's input x [N][H][64][64] ...
   const uint8_t* bn_mask;  // ... its ReLU mask (1 bit / element) and ...
   const float* bn_mean;    // ... its batch mean: out = dgrad * mask, stats = its backward sums
@@ -611,7 +617,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   for (int e = 0; e < (STATS ? 16 : 1); ++e) ls[e] = LaneStat{0.f, 0.f, 0.f};
 
   u32x4 av[NST];  // ACC: the addend pieces of the tile stored next; BNB: the BatchNorm input x there
-  uint32_t bm[BNB ? NST : 1];  // BNB: the mask byte of each piece (8 channels)
+  uint32_t bm[(BNB || ACC) ? NST : 1];  // BNB / masked ACC: the mask byte of each piece (8 channels)
   float bs1[BNB ? 8 : 1], bs2[BNB ? 8 : 1], bmu[BNB ? 8 : 1];  // BNB: this thread's 8 channels (tid & 7)
   if constexpr (BNB) {
 #pragma unroll
@@ -625,6 +631,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     const char* src = (const char*)(BNB ? a.bn_x : a.addend) + tile0 * 2;
     av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
     if constexpr (BNB) bm[q] = a.bn_mask[tile0 / 8 + q * NT + tid];
+    if constexpr (ACC) bm[q] = a.addend_mask ? a.addend_mask[tile0 / 8 + q * NT + tid] : 0xffu;
   };
   // (use = false: a tile that does not exist -- the stores go out of the buffer's range and are
   // dropped; issuing them anyway keeps the vector-memory instruction count the same on every path,
@@ -637,8 +644,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
       if constexpr (ACC) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          v[e] = pack2<T>(lo2f<T>(v[e]) + lo2f<T>(av[q][e]), hi2f<T>(v[e]) + hi2f<T>(av[q][e]));
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t ad = av[q][e] & ((((bm[q] >> (2 * e)) & 1u) ? 0xffffu : 0u) |
+                                          (((bm[q] >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u));
+          v[e] = pack2<T>(lo2f<T>(v[e]) + lo2f<T>(ad), hi2f<T>(v[e]) + hi2f<T>(ad));
+        }
       }
       if constexpr (BNB) {
 #pragma unroll
@@ -1615,7 +1625,9 @@ bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
 }  // namespace
 
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
-                 float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb, int stride) {
+                 float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb, int stride,
+                 const uint8_t* addend_mask) {
+  if (addend_mask && (!addend || stride != 1)) return kNotHandled;
   if (g_direct == 0) return kNotHandled;
   if (stride == 2) {  // forward only (H, W: the input size)
     if (flip || addend || bnb || H % 2 || W % 2 || Cin % 64 || Nout % 64) return kNotHandled;
@@ -1677,6 +1689,7 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     p.w = w;
     p.out = out;
     p.addend = addend;
+    p.addend_mask = addend_mask;
     p.bn_x = bnb ? bnb->x : nullptr;
     p.bn_mask = bnb ? bnb->mask : nullptr;
     p.bn_mean = bnb ? bnb->mean : nullptr;
@@ -1712,6 +1725,7 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   a.w = w;
   a.out = out;
   a.addend = addend;
+  a.addend_mask = addend_mask;
   a.bn_x = bnb ? bnb->x : nullptr;
   a.bn_mask = bnb ? bnb->mask : nullptr;
   a.bn_mean = bnb ? bnb->mean : nullptr;

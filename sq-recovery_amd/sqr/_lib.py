@@ -99,6 +99,8 @@ SIGNATURES = {
                                     c_size_t, c_void_p]),
     "sqr_conv2d_bwd_data_acc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),
                                         c_void_p, c_size_t, c_void_p]),
+    "sqr_conv2d_bwd_data_acc_masked": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_data_acc_s2": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),
                                            c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_data_bn_stats_floats": (c_size_t, [ctypes.POINTER(SqrConvDesc)]),

@@ -12,6 +12,7 @@ import torch
 
 from . import gradbuf
 from ._lib import SqrBnOperand, check, lib, ptr, stream_ptr
+from .conv import MaskedGrad
 
 _CL = torch.channels_last
 
@@ -98,7 +99,12 @@ class BNActFn(torch.autograd.Function):
             return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None, None, \
                 None, None
         dx = torch.empty_like(x, memory_format=_CL)
-        dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5]) else None
+        # an identity block's residual share g = dy * mask goes to conv1's backward-data as (dy, mask)
+        # (sqr.conv.MaskedGrad) instead of being written here, when conv1's backward is still to run
+        masked = (ctx.has_res and ctx.needs_input_grad[5] and ctx.res_join is not None and ym is not None
+                  and x.dtype in (torch.bfloat16, torch.float16) and ctx.res_join.will_take())
+        dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.needs_input_grad[5] and not masked) \
+            else None
         dgamma = gradbuf.out(ctx.pids[0], (C,), x.device)
         dbeta = gradbuf.out(ctx.pids[1], (C,), x.device)
         n = _ws_bytes(M, C)
@@ -109,7 +115,9 @@ class BNActFn(torch.autograd.Function):
                                         ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta),
                                         ptr(ws), n, stream_ptr(x.device)), "sqr_bn_bwd_part")
             gradbuf.written(ctx.pids)
-            if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
+            if masked:
+                dres = MaskedGrad(dy, ym)
+            elif ctx.has_res and dres is None and ctx.needs_input_grad[5]:
                 dres = dy
             if ctx.res_join is not None:
                 dres = ctx.res_join.deposit(dres)
@@ -131,7 +139,9 @@ class BNActFn(torch.autograd.Function):
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
         gradbuf.written(ctx.pids)
-        if ctx.has_res and dres is None and ctx.needs_input_grad[5]:
+        if masked:
+            dres = MaskedGrad(dy, ym)
+        elif ctx.has_res and dres is None and ctx.needs_input_grad[5]:
             dres = dy
         if ctx.res_join is not None:
             dres = ctx.res_join.deposit(dres)

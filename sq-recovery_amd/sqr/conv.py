@@ -402,6 +402,24 @@ class BnOutLink:
         return part, rows.value
 
 
+class MaskedGrad:
+    """A ReLU-masked gradient g = dy * [mask bit] kept as (dy, mask) (1 bit per element, NHWC order):
+    an identity block's residual share deposited in a ResidualJoin without writing g; conv1's
+    direct backward-data masks it while adding (sqr_conv2d_bwd_data_acc_masked), any other consumer
+    gets full()."""
+
+    __slots__ = ("dy", "mask", "shape")
+
+    def __init__(self, dy, mask):
+        self.dy, self.mask, self.shape = dy, mask, tuple(dy.shape)
+
+    def full(self):
+        N, C, H, W = self.shape
+        bits = (self.mask.view(-1, 1) >> torch.arange(8, device=self.mask.device, dtype=torch.uint8)) & 1
+        nhwc = self.dy.permute(0, 2, 3, 1) * bits.view(N, H, W, C).to(self.dy.dtype)
+        return nhwc.permute(0, 3, 1, 2).contiguous(memory_format=_CL)
+
+
 class ResidualJoin:
     """The two gradient contributions of a residual block's input x (torchvision BasicBlock:
     x feeds conv1 AND the identity / downsample branch, torch/models.py:181) summed without a
@@ -433,11 +451,15 @@ class ResidualJoin:
             return None
         if self.acc_done:  # conv1's backward already ran: autograd adds this one
             self.acc_done = False
-            return g
+            return g.full() if isinstance(g, MaskedGrad) else g
         self.pending = g
         if torch._C._current_graph_task_id() != -1:  # inside a backward pass (always, in the model)
             torch.autograd.Variable._execution_engine.queue_callback(self._check_taken)
         return None
+
+    def will_take(self):
+        """True while conv1's backward has not run in this pass (a deposit now is taken by it)."""
+        return not self.acc_done
 
     def _check_taken(self):
         if self.pending is not None:
@@ -453,6 +475,20 @@ class ResidualJoin:
         else:
             self.acc_done = False
         return g
+
+
+class _MaskedDone:
+    """conv1's backward-data already added a MaskedGrad (the result dx)."""
+
+    __slots__ = ("dx",)
+
+    def __init__(self, dx):
+        self.dx = dx
+
+
+def ctypes_ref(d):
+    import ctypes
+    return ctypes.byref(d)
 
 
 def compute_dtype(x):
@@ -518,6 +554,21 @@ class Conv2dFn(torch.autograd.Function):
             if crsk is None:
                 raise RuntimeError("sqr conv: backward-data for C<8 inputs is not supported")
             addend = ctx.join.take() if (ctx.join is not None and ctx.role == "acc") else None
+            if isinstance(addend, MaskedGrad):
+                if (addend.dy.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W) and d.R == 3 and d.S == 3
+                        and d.stride == 1 and d.pad == 1 and addend.dy.is_contiguous(memory_format=_CL)):
+                    dx = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=g.device, memory_format=_CL)
+                    ws, n = _ws(d, 1, g.device)
+                    with _Probe("dgrad", d):
+                        rc = lib().sqr_conv2d_bwd_data_acc_masked(ptr(g), ptr(crsk), ptr(dx), ptr(addend.dy),
+                                                                  ptr(addend.mask), ctypes_ref(d), ptr(ws), n,
+                                                                  stream_ptr(g.device))
+                    if rc == 0:
+                        addend = _MaskedDone(dx)
+                    elif rc != -2:  # (-2: SQR_E_UNSUPPORTED -> mask, then the plain paths below)
+                        check(rc, "sqr_conv2d_bwd_data_acc_masked")
+                if isinstance(addend, MaskedGrad):
+                    addend = addend.full()
             s2 = isinstance(addend, CompactS2)
             if s2 and not (d.stride == 2 and addend.t.dtype == dt and addend.shape == (d.N, d.C, d.H, d.W)
                            and tuple(addend.t.shape) == (d.N, d.C, d.H // 2, d.W // 2) and d.H % 2 == 0
@@ -527,6 +578,9 @@ class Conv2dFn(torch.autograd.Function):
             if link is not None and link.x.dtype == dt:
                 dx, link.stats = conv2d_bwd_data_bn(g, crsk, d, link.x, link.mask, link.mean)
                 link.g = dx
+            elif isinstance(addend, _MaskedDone):
+                dx = addend.dx
+                ride_red = ctx.bnr  # dx is the whole gradient of x: its BatchNorm reduction can ride
             elif s2:
                 dx = conv2d_bwd_data_acc_s2(g, crsk, d, addend.t)
                 ride_red = ctx.bnr  # dx is the whole gradient of x: its BatchNorm reduction can ride

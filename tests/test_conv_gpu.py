@@ -481,6 +481,52 @@ def test_conv_bwd_data_acc(shape, dtype):
     assert torch.equal(addg.cpu().float(), add.to(dtype).float())  # the addend is not modified
 
 
+# sqr_conv2d_bwd_data_acc_masked: the addend is an identity block's ReLU-masked gradient kept as
+# (dy, mask) (sqr.conv.MaskedGrad); must equal the ACC launch on the materialised masked tensor
+# bitwise (masked-out halves are +0 either way), and float64 within the 16-bit tolerance.
+MASKED_SHAPES = [(4, 64, 64, 64), (64, 64, 64, 64), (4, 128, 32, 128), (4, 256, 16, 256), (4, 512, 8, 512),
+                 (64, 128, 32, 128), (64, 512, 8, 512)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("shape", MASKED_SHAPES, ids=lambda s: "N%dC%dH%dK%d" % s)
+def test_conv_bwd_data_acc_masked(shape, dtype):
+    import ctypes
+    from sqr import conv as sc
+    from sqr._lib import lib, ptr, stream_ptr
+    N, C, H, K = shape
+    g = torch.Generator().manual_seed(7 * N + C + K)
+    w = torch.randn(K, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    gy = torch.randn(N, K, H, H, generator=g).to(dtype).float()
+    dy = torch.randn(N, C, H, H, generator=g).to(dtype).float()
+    keep = torch.rand(N, H, H, C, generator=g) > 0.4  # NHWC element order, as the ReLU mask
+    bits = keep.reshape(-1, 8).to(torch.uint8)
+    mask = (bits << torch.arange(8, dtype=torch.uint8)).sum(dim=1, dtype=torch.uint8)
+    d = sc._desc(N, C, H, H, K, 3, 3, 1, 1, dtype)
+    _, crsk = sc.pack_weight(w.to(DEV), d, True)
+    gyg = gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    dyg = dy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    mg = sc.MaskedGrad(dyg, mask.to(DEV))
+    full = mg.full()
+    dx = torch.empty((N, C, H, H), dtype=dtype, device=DEV, memory_format=torch.channels_last)
+    ws, n = sc._ws(d, 1, gyg.device)
+    rc = lib().sqr_conv2d_bwd_data_acc_masked(ptr(gyg), ptr(crsk), ptr(dx), ptr(dyg), ptr(mg.mask), ctypes.byref(d),
+                                              ptr(ws), n, stream_ptr(gyg.device))
+    ref_acc = sc.conv2d_bwd_data_acc(gyg, crsk, d, full)
+    torch.cuda.synchronize()
+    masked_ref = dy * keep.permute(0, 3, 1, 2).float()
+    assert torch.equal(full.cpu().float(), masked_ref.to(dtype).float())
+    if rc == -2:  # no direct kernel at this size (too few tiles): sqr.conv masks (full()) and adds
+        assert b"masked addend" in lib().sqr_last_error_string()
+        assert N < 64
+        return
+    assert rc == 0, lib().sqr_last_error_string()
+    assert torch.equal(dx, ref_acc)
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w.to(dtype).double(), gy.double(), stride=1, padding=1)
+    ref = ref + masked_ref.double()
+    assert _rel(dx, ref) <= {torch.bfloat16: 1.2e-2, torch.float16: 2e-3}[dtype]
+
+
 # ---------------------------------------------------------------- dgrad + BatchNorm-backward sums
 # sqr_conv2d_bwd_data_bn (a BasicBlock's conv2 backward-data feeding bn1's backward): g = dgrad * mask
 # and the per-channel sums (sum g, sum g*(x - mean)) — the persistent layer-1 kernel (ring wrap at
