@@ -92,17 +92,13 @@ class Trainer:
         self.gdp = None
         self.model = self.net
         # dp_rehearsal: the N>1 path (flat buffer, bucket hooks, captured RCCL all-reduce) at N=1 on a
-        # world-1 RCCL group
-        if dp_rehearsal and world == 1 and not torch.distributed.is_initialized():
-            torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get(
-                "MASTER_PORT", "29517"), rank=0, world_size=1, device_id=dev)
-        if (world > 1 or dp_rehearsal) and graph:
+        # world-1 libsqr RCCL communicator
+        if dp_rehearsal and world == 1:
+            dist.open_comm(dev)
+        if world > 1 or dp_rehearsal:
+            # the same data path captured (default) or eager (--graph 0); no other fallback
             self.gdp = dist.GraphDataParallel(self.net, self.opt, dev)
-        elif world > 1:
-            self.model = dist.wrap(self.net, dev)
-            self.use_graph = False
         self.grad_seed = torch.ones((), dtype=torch.float64, device=dev)
-        self.dp_note = None
         self.graph = None
         self.static_loss = None
         self._step = self.eager_step
@@ -138,7 +134,6 @@ class Trainer:
         int64 [n, 2] device tensor; the probed conv's launches captured in the graph record their
         wall-clock spans into its rows on every replay (sqr_probe_arm_clock)."""
         from sqr import conv as sconv
-        from sqr import dist
         if not self.use_graph:
             return
         side = torch.cuda.Stream()
@@ -154,24 +149,10 @@ class Trainer:
         if probe_clock is not None:
             sconv.set_probe(*self.probe_key(), clock=probe_clock)
         try:
-            # thread_local: ProcessGroupNCCL's watchdog thread polls the events of the eager warm-up
-            # all-reduces; under the default "global" mode such a poll from another thread during the
-            # capture is an unsafe call (hipErrorStreamCaptureUnsupported), the watchdog rethrows and the
-            # process aborts (tests/test_dp_graph_gpu.py)
+            # thread_local: a capture-unsafe HIP call from another thread (RCCL's proxy thread) is not
+            # an error for this capture
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 self.static_loss = self.body()
-        except Exception as e:  # N > 1 only: keep the run alive on eager DDP (reported in "dp")
-            if self.gdp is None:
-                raise
-            self.dp_note = "capturing the data-parallel step failed (%s: %s); eager DDP instead" % (
-                type(e).__name__, e)
-            print("bench: " + self.dp_note, file=sys.stderr)
-            torch.cuda.synchronize()
-            self.gdp.close(self.opt)
-            self.gdp = None
-            self.model = dist.wrap(self.net, self.dev)
-            self.use_graph = False
-            return
         finally:
             if probe_clock is not None:
                 self.probe_rows = sconv.probe_clock_rows()
@@ -422,16 +403,26 @@ def main():
     os.dup2(2, 1)
 
     from sqr import dist
-    rank, world, dev = dist.init("nccl")
-    dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype)
-    tr = Trainer(dev, config=args.config, batch=args.batch, render=args.render, dtype=dtype,
-                 graph=args.graph != 0, rank=rank, world=world, dp_rehearsal=args.dp_rehearsal)
-    B, H, R = tr.B, tr.H, tr.R
-    probe_clock = None
-    if tr.use_graph and not args.profile:
-        probe_clock = torch.empty(N_PROBE_SLOTS, 2, dtype=torch.int64, device=dev)
-        _clock_reset(probe_clock)
-    tr.capture(probe_clock)
+    rank, world = dist.env()[:2]
+    try:
+        rank, world, dev = dist.init("nccl")
+        dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype)
+        tr = Trainer(dev, config=args.config, batch=args.batch, render=args.render, dtype=dtype,
+                     graph=args.graph != 0, rank=rank, world=world, dp_rehearsal=args.dp_rehearsal)
+        B, H, R = tr.B, tr.H, tr.R
+        probe_clock = None
+        if tr.use_graph and not args.profile:
+            probe_clock = torch.empty(N_PROBE_SLOTS, 2, dtype=torch.int64, device=dev)
+            _clock_reset(probe_clock)
+        tr.capture(probe_clock)
+    except Exception as e:
+        # no silent fallback: the data path (communicator self-test, capture) failed -> one JSON line
+        # naming the cause, and a non-zero exit
+        if rank == 0:
+            os.write(json_fd, (json.dumps({"metric": "training images/sec", "value": None, "unit": "images/s",
+                                           "n_gpus": world, "dp_error": "%s: %s" % (type(e).__name__, e)})
+                               + "\n").encode())
+        raise
 
     # dist.barrier: every rank's GPU work drained, then a host (gloo) barrier — no eager collective
     # ever runs on the RCCL communicator that the captured step's all-reduces use
@@ -463,9 +454,9 @@ def main():
                       "per_gpu_batch": B, "image": "%dx%dx1" % (H, H), "render_size": R,
                       "parallelism": "dp%d" % world},
            "final_loss": final_loss, "hip_graph": tr.use_graph,
-           "dp": ("graph-captured RCCL all-reduce" if tr.gdp is not None else ("DDP" if world > 1 else None))}
-    if tr.dp_note:
-        out["dp_note"] = tr.dp_note
+           "dp": (("%s bucketed RCCL all-reduce on a side stream (libsqr communicator, RCCL %d)"
+                   % ("graph-captured" if tr.graph is not None else "eager", dist.comm().version))
+                  if tr.gdp is not None and dist.comm() is not None else None)}
     if tr.scaler is not None:
         out["loss_scale"] = float(tr.scaler.get_scale())
 

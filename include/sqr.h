@@ -30,6 +30,8 @@
  *   sqr_amp_*, sqr_adam_step_amp  torch.amp.GradScaler around that step (fp16 config 5; the reference
  *                              trains fp32 and has no scaler — this is the scaler torch pairs with fp16).
  *   sqr_tail_fwd / _bwd        ResNetSQ avgpool + encoder.fc + output heads (torch/models.py:7-99,186-204).
+ *   sqr_comm_*                 the gradient all-reduce a DistributedDataParallel wrap of train.py's net
+ *                              (torch/train.py:43) would issue, on a libsqr-owned RCCL communicator.
  */
 #ifndef SQR_H
 #define SQR_H
@@ -441,6 +443,32 @@ typedef struct sqr_tail_grads {
 size_t sqr_tail_workspace_bytes(const sqr_tail_desc* t);
 int sqr_tail_bwd(const sqr_tail_desc* t, const float* save, const sqr_tail_grads* g, void* workspace,
                  size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------- data-parallel gradient exchange
+ * One RCCL communicator per rank, owned by libsqr (not by torch's ProcessGroupNCCL), carrying the
+ * bucketed gradient all-reduce of a data-parallel step (north_star: "RCCL all-reduce
+ * of gradients over xGMI overlapped with backward on a side HIP stream").  The reference trains on one
+ * GPU (torch/train.py:42-54); these calls replace what a DistributedDataParallel wrap around its
+ * `net` (train.py:43) would issue.  The collectives are stream-ordered and graph-capturable: a
+ * captured step holds plain RCCL kernels and no host-side completion tracking (no watchdog).
+ *   sqr_comm_load        dlopen the process's RCCL (path, NULL = "librccl.so.1", i.e. the copy
+ *                        already mapped by torch); *version = ncclGetVersion (nullable);
+ *   sqr_comm_unique_id   rank 0: a fresh SQR_COMM_ID_BYTES id, to be sent to every rank (host group);
+ *   sqr_comm_init_rank   collective over all ranks, on the calling thread's current HIP device;
+ *   sqr_comm_allreduce_sum_f32  in-place sum of count floats over the ranks;
+ *   sqr_comm_broadcast   in-place byte broadcast from root (parameter / buffer init);
+ *   sqr_comm_async_error 0, or the communicator's asynchronous failure as an error;
+ *   sqr_comm_destroy     finalize + destroy (after every graph holding its collectives is destroyed).
+ * Errors from RCCL are returned as 1000 + ncclResult_t. */
+#define SQR_COMM_ID_BYTES 128
+typedef struct sqr_comm* sqr_comm_t;
+int sqr_comm_load(const char* rccl_path, int* version);
+int sqr_comm_unique_id(unsigned char* id_out);
+int sqr_comm_init_rank(sqr_comm_t* comm, const unsigned char* id, int nranks, int rank);
+int sqr_comm_allreduce_sum_f32(sqr_comm_t comm, float* buf, size_t count, void* stream);
+int sqr_comm_broadcast(sqr_comm_t comm, void* buf, size_t bytes, int root, void* stream);
+int sqr_comm_async_error(sqr_comm_t comm);
+int sqr_comm_destroy(sqr_comm_t comm);
 
 #ifdef __cplusplus
 }

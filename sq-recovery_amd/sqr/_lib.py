@@ -171,6 +171,13 @@ SIGNATURES = {
     "sqr_tail_workspace_bytes": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_bwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, ctypes.POINTER(SqrTailGrads), c_void_p,
                              c_size_t, c_void_p]),
+    "sqr_comm_load": (c_int, [ctypes.c_char_p, ctypes.POINTER(c_int)]),
+    "sqr_comm_unique_id": (c_int, [c_void_p]),
+    "sqr_comm_init_rank": (c_int, [ctypes.POINTER(c_void_p), c_void_p, c_int, c_int]),
+    "sqr_comm_allreduce_sum_f32": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "sqr_comm_broadcast": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "sqr_comm_async_error": (c_int, [c_void_p]),
+    "sqr_comm_destroy": (c_int, [c_void_p]),
 }
 
 

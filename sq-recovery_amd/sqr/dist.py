@@ -1,19 +1,27 @@
 """Data-parallel plumbing shared by train.py and bench.py.
 
-One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE), backend
-"nccl" = RCCL over xGMI on ROCm (gloo for CPU runs).  Images are independent, so the only data-path
-collective is the gradient all-reduce, bucketed and overlapped with backward by GraphDataParallel
-(below); BatchNorm keeps per-rank batch statistics (the reference trains on one GPU; DDP without
-SyncBN is the documented multi-GPU semantics: an N-rank step equals the average of N independent
-per-rank gradients).  ``wrap`` (torch DDP) remains as the fallback when a step cannot be captured.
+One process per GPU (torchrun / torch.distributed.run sets RANK, LOCAL_RANK, WORLD_SIZE).  Images
+are independent, so the only data-path collective is the gradient all-reduce, bucketed and
+overlapped with backward by GraphDataParallel (below).  It runs on an RCCL communicator that libsqr
+owns (``Comm``: sqr_comm_* in include/sqr.h, RCCL over xGMI), NOT on torch's ProcessGroupNCCL:
+a collective issued through ProcessGroupNCCL becomes a Work whose end event the PG's watchdog thread
+polls, and when that event was recorded inside the captured step graph the poll fails
+(hipErrorCapturedEvent) and the watchdog aborts the process (round 3, tests/test_dp_graph_gpu.py).
+The captured step now holds plain RCCL kernels and nothing on the host tracks them.
+
+torch.distributed keeps a gloo process group for host-side work only: the unique-id exchange of
+the communicator, barriers, and the timing / logging reductions.  BatchNorm keeps per-rank batch
+statistics (the reference trains on one GPU; DDP without SyncBN is the documented multi-GPU
+semantics: an N-rank step equals the average of N independent per-rank gradients).
 """
+import ctypes
 import gc
 import os
 
 import torch
 import torch.distributed as dist
 
-# DDP bucket size: 45.5 MB of fp32 ResNetSQ gradients -> 3 buckets; large enough that each ring
+# gradient bucket size: 45.5 MB of fp32 ResNetSQ gradients -> 3 buckets; large enough that each ring
 # all-reduce runs near xGMI link bandwidth, small enough that the first bucket (layer4 + heads)
 # starts while layer3..layer1 backward still runs.
 BUCKET_MB = 16
@@ -25,46 +33,124 @@ def env():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-# Host-side synchronisation (barriers, timing / logging reductions) runs on a gloo group of its
-# own, never on the RCCL communicator: that communicator carries only the gradient all-reduces,
-# which bench.py captures in its step graph.  Eager RCCL collectives issued after a graph with
-# captured RCCL work was replayed or destroyed are what aborted inside RCCL in round 2 (a
-# tdist.barrier() right after CUDAGraph.reset()); with the host group the communicator sees no
-# eager work after the first capture, and its teardown (finish) follows the ordered sequence below.
-_host = [None]
-
-
 def host_group():
-    """The gloo group for host-side collectives (the default group when that is gloo already).
-    Created on first use; every rank reaches it through the same collective calls."""
+    """The process group for host-side collectives: the default group, which is gloo (the data
+    path's RCCL traffic never goes through torch.distributed)."""
     if not dist.is_initialized():
         return None
-    if dist.get_backend() == "gloo":
-        return dist.group.WORLD
-    if _host[0] is None:
-        _host[0] = dist.new_group(backend="gloo")
-    return _host[0]
+    return dist.group.WORLD
+
+
+def _torch_rccl_path():
+    """The librccl torch itself maps (its bundled copy), so the process holds ONE RCCL runtime."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else None
+
+
+class Comm:
+    """libsqr's RCCL communicator (sqr_comm_*): world ranks, one per GPU, created collectively on
+    the current device.  The unique id goes from rank 0 to the others over the host group."""
+
+    def __init__(self, rank, world):
+        from ._lib import check, lib
+        L = lib()
+        ver = ctypes.c_int(0)
+        path = _torch_rccl_path()
+        check(L.sqr_comm_load(path.encode() if path else None, ctypes.byref(ver)), "sqr_comm_load")
+        uid = (ctypes.c_ubyte * 128)()
+        if rank == 0:
+            check(L.sqr_comm_unique_id(uid), "sqr_comm_unique_id")
+        if world > 1:
+            t = torch.tensor(list(bytes(uid)), dtype=torch.uint8)
+            dist.broadcast(t, 0, group=host_group())
+            uid = (ctypes.c_ubyte * 128)(*t.tolist())
+        h = ctypes.c_void_p()
+        check(L.sqr_comm_init_rank(ctypes.byref(h), uid, world, rank), "sqr_comm_init_rank")
+        self.handle, self.rank, self.world, self.version = h, rank, world, ver.value
+
+    def allreduce_(self, t, stream=None):
+        """In-place sum of a contiguous fp32 CUDA tensor over the ranks, on `stream` (default: the
+        current stream); capturable."""
+        from ._lib import check, lib
+        assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous(), "allreduce_: contiguous fp32 CUDA"
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        check(lib().sqr_comm_allreduce_sum_f32(self.handle, ctypes.c_void_p(t.data_ptr()), t.numel(),
+                                               ctypes.c_void_p(s)), "sqr_comm_allreduce_sum_f32")
+
+    def broadcast_(self, t, root=0):
+        """In-place broadcast of a contiguous CUDA tensor (any dtype) from `root`."""
+        from ._lib import check, lib
+        assert t.is_cuda and t.is_contiguous(), "broadcast_: contiguous CUDA tensor"
+        check(lib().sqr_comm_broadcast(self.handle, ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(),
+                                       root, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+              "sqr_comm_broadcast")
+
+    def check(self):
+        """Raise if the communicator reported an asynchronous failure."""
+        from ._lib import check, lib
+        check(lib().sqr_comm_async_error(self.handle), "sqr_comm_async_error")
+
+    def selftest(self, device):
+        """Eager all-reduce of rank+1 (sum must be world(world+1)/2): run once before any capture, so
+        a broken communicator fails here, loudly, not inside a replayed graph."""
+        t = torch.full((1024,), float(self.rank + 1), dtype=torch.float32, device=device)
+        self.allreduce_(t)
+        torch.cuda.synchronize(device)
+        self.check()
+        want = self.world * (self.world + 1) / 2
+        if not bool((t == want).all()):
+            raise RuntimeError("sqr.dist.Comm self-test: all-reduce gave %r, expected %r" % (t[0].item(), want))
+
+    def destroy(self):
+        from ._lib import check, lib
+        h, self.handle = self.handle, None
+        if h is not None:
+            check(lib().sqr_comm_destroy(h), "sqr_comm_destroy")
+
+
+_comm = [None]
+
+
+def comm():
+    """The data-parallel communicator of this process (None: no RCCL data path)."""
+    return _comm[0]
+
+
+def open_comm(device, rank=None, world=None):
+    """Create this process's RCCL communicator (collective over the ranks when world > 1) and
+    self-test it.  With no process group it is a world-1 communicator: bench.py --dp-rehearsal and
+    the GPU tests run the whole N>1 data path (captured all-reduce included) on one GPU."""
+    if _comm[0] is None:
+        if rank is None:
+            rank, world = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+        c = Comm(rank, world)
+        _comm[0] = c
+        c.selftest(device)
+    return _comm[0]
 
 
 def init(backend="nccl", device_type=None):
-    """Set this rank's device and join the process group when WORLD_SIZE > 1.
-    Returns (rank, world, device).  backend "gloo" with device_type "cuda" keeps the GPU path on a
+    """Set this rank's device and join the process group when WORLD_SIZE > 1.  Returns (rank,
+    world, device).  backend "nccl": the data path runs over RCCL (libsqr's communicator, one GPU per
+    rank), the host group is gloo.  backend "gloo" with device_type "cuda" keeps the GPU path on the
     gloo group (several ranks on one GPU: the multi-rank GPU tests; RCCL refuses duplicate GPUs)."""
     rank, world, local = env()
     device_type = device_type or ("cuda" if backend == "nccl" else "cpu")
     if device_type == "cuda":
-        ndev = torch.cuda.device_count()
-        idx = local % ndev if ndev else local
+        if backend == "gloo":
+            # several ranks may share the test box's GPU
+            ndev = torch.cuda.device_count()
+            idx = local % ndev if ndev else local
+        else:
+            idx = local  # one GPU per rank: an out-of-range LOCAL_RANK fails here, clearly
         torch.cuda.set_device(idx)
         device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
-        host_group()
+        dist.init_process_group("gloo")
+    if world > 1 and backend == "nccl" and device.type == "cuda":
+        open_comm(device, rank, world)
     return rank, world, device
 
 
@@ -80,16 +166,6 @@ def shard(n, rank, world):
     return range(rank * per, (rank + 1) * per)
 
 
-def wrap(model, device):
-    """DistributedDataParallel with the bucket layout above (identity when not distributed)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
-        return model
-    from torch.nn.parallel import DistributedDataParallel as DDP
-    ids = [device.index] if device.type == "cuda" else None
-    return DDP(model, device_ids=ids, bucket_cap_mb=BUCKET_MB, gradient_as_bucket_view=True,
-               broadcast_buffers=False)
-
-
 class GraphDataParallel:
     """Data parallelism whose whole step — forward, loss, backward, gradient all-reduce, optimizer —
     can be captured as ONE HIP graph (DDP's reducer cannot be captured, and eager launching of the
@@ -100,8 +176,8 @@ class GraphDataParallel:
     gradients straight into the slots; any other op's gradient is moved into its slot by the
     parameter's post-accumulate-grad hook (the host CPU path, plain torch modules).  The buffer is
     cut into buckets of ~``bucket_mb``; as soon as the backward has produced the last gradient of a
-    bucket, that bucket is summed in place over the ranks (RCCL on a side stream for CUDA,
-    overlapping the rest of the backward; the dependencies are stream events, so they are captured
+    bucket, that bucket is summed in place over the ranks (libsqr's RCCL communicator on a side
+    stream for CUDA, overlapping the rest of the backward; the dependencies are stream events, so they are captured
     with the graph; gloo in-line on the CPU).  ``allreduce()`` (after ``backward``) joins the side
     stream; the fused optimizer averages while it reads (``optimizer.sqr_grad_scale = 1 / world``;
     other optimizers get the buffer scaled once).  Semantics are DDP's: parameters and buffers are
@@ -111,12 +187,20 @@ class GraphDataParallel:
     def __init__(self, model, optimizer, device, bucket_mb=BUCKET_MB):
         from . import gradbuf
         self.model = model
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        device = torch.device(device)
+        # the RCCL communicator when this process has one (CUDA, one GPU per rank), else the
+        # process group (gloo: the host path, or several ranks sharing one GPU)
+        self.comm = comm() if device.type == "cuda" else None
+        self.world = self.comm.world if self.comm is not None else (
+            dist.get_world_size() if dist.is_initialized() else 1)
         self.params = [p for p in model.parameters() if p.requires_grad]
         if self.world > 1:
             with torch.no_grad():
                 for t in list(model.parameters()) + list(model.buffers()):
-                    dist.broadcast(t.data, 0)
+                    if self.comm is not None:
+                        self.comm.broadcast_(t.data)
+                    else:
+                        dist.broadcast(t.data, 0)
         order = list(reversed(self.params))  # the backward produces the last layers' grads first
         self.flat = gradbuf.install(order, device)
         self.param_of = {id(p): p for p in self.params}
@@ -135,7 +219,6 @@ class GraphDataParallel:
         for b, (_, _, mem) in enumerate(self.buckets):
             for pid in mem:
                 self.bucket_of[pid] = b
-        device = torch.device(device)
         self.side = torch.cuda.Stream(device) if device.type == "cuda" else None
         self.launch_log = []  # bucket indices in launch order (tests)
         self._reset()
@@ -157,7 +240,7 @@ class GraphDataParallel:
             return
         self.launched[b] = True
         self.launch_log.append(b)
-        if not dist.is_initialized():
+        if self.comm is None and not dist.is_initialized():
             return
         lo, hi, _ = self.buckets[b]
         view = self.flat[lo:hi]
@@ -165,8 +248,11 @@ class GraphDataParallel:
             dist.all_reduce(view)
             return
         self.side.wait_stream(torch.cuda.current_stream())
+        if self.comm is not None:
+            self.comm.allreduce_(view, self.side)  # SUM in place; the optimizer scales by 1 / world
+            return
         with torch.cuda.stream(self.side):
-            dist.all_reduce(view)  # SUM in place; the optimizer scales by 1 / world
+            dist.all_reduce(view)
 
     def _mark(self, pid):
         if pid in self.done:
@@ -238,9 +324,10 @@ class GraphDataParallel:
 
 
 def capturable():
-    """Whether the gradient all-reduce can be captured in a HIP graph: RCCL (or no process group);
-    gloo all-reduces of CUDA tensors go through the host and run eagerly only."""
-    return not (dist.is_initialized() and dist.get_world_size() > 1 and dist.get_backend() != "nccl")
+    """Whether the gradient all-reduce can be captured in a HIP graph: with the RCCL communicator
+    (or no data-parallel peers); gloo all-reduces of CUDA tensors go through the host and run
+    eagerly only."""
+    return comm() is not None or not (dist.is_initialized() and dist.get_world_size() > 1)
 
 
 def _multi():
@@ -281,7 +368,8 @@ def barrier():
 def finish(*graphs):
     """Ordered teardown: drain the device; destroy the step graphs (the RCCL plans captured in them
     are released with the graph, and must be before their communicator goes); drain again; wait for
-    every rank on the host group; only then destroy the process groups (RCCL communicator included)."""
+    every rank on the host group; destroy the RCCL communicator; wait again; only then destroy the
+    process group."""
     if _cuda_live():
         torch.cuda.synchronize()
     for g in graphs:
@@ -290,8 +378,12 @@ def finish(*graphs):
     gc.collect()
     if _cuda_live():
         torch.cuda.synchronize()
-    if dist.is_initialized():
-        if dist.get_world_size() > 1:
+    if _multi():
+        dist.barrier(group=host_group())
+    c, _comm[0] = _comm[0], None
+    if c is not None:
+        c.destroy()
+        if _multi():
             dist.barrier(group=host_group())
+    if dist.is_initialized():
         dist.destroy_process_group()
-    _host[0] = None

@@ -13,7 +13,10 @@ Adam (and the fp16 loss scaler) — is captured once and replayed per batch:
   waits for the host;
 * the optimizer's learning rates are kernel arguments of the captured Adam launch: a change (the
   reference's ReduceLROnPlateau) recaptures the graph;
-* a batch of a different shape (the epoch's partial last batch) runs the same step eagerly.
+* a batch of a different shape (the epoch's partial last batch) runs the same step eagerly; under
+  data parallelism its all-reduces are eager RCCL calls on the communicator the graph's captured
+  all-reduces use (libsqr's own, sqr.dist.Comm: no host-side tracking of either kind), issued in the
+  same order on every rank because every rank runs the same sequence of batch shapes.
 
 The first batch runs eagerly (it initialises the optimizer state, the packed weights and the
 gradient buffers outside the capture); every batch is trained exactly once, as in the reference.
@@ -57,7 +60,12 @@ class CapturedStep:
         return self._pair(self.body(x, y))
 
     def _capture(self, x, y, key):
-        self.graph = None
+        old, self.graph = self.graph, None
+        if old is not None:
+            # a recapture (new learning rates): the old graph may still be running and holds captured
+            # all-reduces on the communicator — drain, then destroy it, as sqr.dist.finish does
+            torch.cuda.synchronize(self.device)
+            old.reset()
         self.static_x = x.detach().clone()
         self.static_y = y.detach().clone()
         self.zero_grad()

@@ -15,10 +15,10 @@ MI355X-specific:
   * --bf16 / --fp16 run the network under autocast (fp16 with sqr.amp.GradScaler loss scaling); the
     loss kernels always consume fp32 params;
   * data parallel: launch with `torchrun --nproc-per-node 8 train.py ...` — one process per GPU,
-    sqr.dist.GraphDataParallel (the same bucketed RCCL all-reduce, overlapped with backward, that
-    bench.py captures in its step graph; run eagerly here because the loop reads the loss every
-    step), each rank trains on its own contiguous shard (sqr.dist.shard), rank 0 logs and writes
-    checkpoints (un-prefixed state-dict keys);
+    sqr.dist.GraphDataParallel (the bucketed all-reduce on libsqr's RCCL communicator, overlapped
+    with backward, captured in the step graph below as in bench.py), each rank trains on its own
+    contiguous shard (sqr.dist.shard), rank 0 logs and writes checkpoints (un-prefixed state-dict
+    keys); --dp-rehearsal runs that path on one GPU with a world-1 communicator;
   * --synthetic N trains on N rendered SQ images (no dataset files needed); otherwise the
     reference's H5Dataset(dataset_location, parse_csv(labels), 0.9) is used (needs h5py);
   * on CUDA the whole training step (forward, loss, backward, all-reduce, Adam / loss scaler) is
@@ -73,8 +73,11 @@ def parse_args(argv=None):
     ap.add_argument("--max-steps", type=int, default=0, help="stop an epoch after this many steps (0 = all)")
     ap.add_argument("--graph", type=int, default=1, help="capture the training step in a HIP graph (CUDA; 0 = eager)")
     ap.add_argument("--dist-backend", default="", choices=("", "nccl", "gloo"),
-                    help="process-group backend (default: nccl on CUDA, gloo on CPU; gloo on CUDA runs several "
-                         "ranks on one GPU)")
+                    help="data-path backend (default: nccl on CUDA = libsqr's RCCL communicator, one GPU per rank, "
+                         "host group gloo; gloo on CPU; gloo on CUDA runs several ranks on one GPU, eagerly)")
+    ap.add_argument("--dp-rehearsal", action="store_true",
+                    help="one CUDA rank: run the N>1 data path (flat gradient buffer, bucketed all-reduce on "
+                         "libsqr's RCCL communicator, captured in the step graph) on a world-1 communicator")
     return ap.parse_args(argv)
 
 
@@ -124,7 +127,9 @@ def main(argv=None):
         starting_epoch, net, optimizer, _ = load_model(args.model_location, net, optimizer, scaler=scaler)
     # N > 1: bucketed gradient all-reduce overlapped with backward (the same machinery bench.py
     # captures in its step graph); the model itself stays unwrapped (checkpoints keep plain keys)
-    gdp = dist.GraphDataParallel(net, optimizer, device) if world > 1 else None
+    if args.dp_rehearsal and world == 1 and use_cuda:
+        dist.open_comm(device)
+    gdp = dist.GraphDataParallel(net, optimizer, device) if (world > 1 or dist.comm() is not None) else None
     model = net
 
     implicit = ImplicitLoss(args.render_size, device, 1.5, 260)

@@ -40,3 +40,21 @@ def test_argument_validation_without_gpu():
     assert L.sqr_stem_fused_supported(2, 512, 512) == 1
     assert L.sqr_stem_fused_supported(2, 64, 63) == 0  # conv1 width 32, but W % 4 != 0
     assert L.sqr_stem_fused_supported(2, 64, 96) == 0  # conv1 width 48
+
+
+def test_comm_binds_torch_rccl_without_gpu():
+    """sqr_comm_load binds the RCCL torch maps (no GPU needed for the version / unique id); the
+    collective entry points reject a null communicator on the host."""
+    import ctypes
+    from sqr import _lib, dist
+    L = _lib.lib()
+    ver = ctypes.c_int(0)
+    path = dist._torch_rccl_path()
+    assert L.sqr_comm_load(path.encode() if path else None, ctypes.byref(ver)) == 0, L.sqr_last_error_string()
+    assert ver.value >= 20000  # NCCL-style version code, e.g. 22606
+    uid = (ctypes.c_ubyte * 128)()
+    assert L.sqr_comm_unique_id(uid) == 0, L.sqr_last_error_string()
+    assert any(bytes(uid))
+    assert L.sqr_comm_allreduce_sum_f32(None, None, 0, None) == -1
+    assert b"null communicator" in L.sqr_last_error_string()
+    assert L.sqr_comm_destroy(None) == 0

@@ -2,10 +2,8 @@
 
 * sqr.dist.shard: equal, disjoint, contiguous shards;
 * sqr.dist.max_over_ranks / mean_over_ranks (bench.py timing, train.py logging);
-* a DDP step wrapped exactly as bench.py / train.py wrap it (sqr.dist.wrap: bucket_cap_mb,
-  gradient_as_bucket_view, no buffer broadcast) equals the average of the per-rank independent
-  gradients — the documented N-GPU semantics (per-rank BatchNorm statistics) — checked on the
-  oracle's CPU ResNetSQ (the HIP model needs a GPU; the DDP wiring is model-agnostic);
+* torch's DDP step (the semantics the data path reproduces: per-rank BatchNorm statistics)
+  equals the average of the per-rank independent gradients, on the oracle's CPU ResNetSQ;
 * helpers.save_model on the DDP-wrapped model writes un-prefixed keys that load into a bare model;
 * sqr.dist.GraphDataParallel — the data-parallel path of bench.py (captured) and train.py (eager) —
   on the PRODUCT ResNetSQ (its host-CPU path): the real backward drives the bucket all-reduces
@@ -61,7 +59,8 @@ def _worker(rank, world, port, tmpdir, q):
         net = ref_torch.ResNetSQRef()
         ref = ref_torch.ResNetSQRef()
         ref.load_state_dict(net.state_dict())
-        model = sd.wrap(net, dev)
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        model = DDP(net, bucket_cap_mb=sd.BUCKET_MB, gradient_as_bucket_view=True, broadcast_buffers=False)
         assert model is not net
         g = torch.Generator().manual_seed(11)
         batches = [torch.rand(2, 1, 64, 64, generator=g) for _ in range(world)]

@@ -1,13 +1,14 @@
-"""Graph-captured data parallelism (sqr.dist.GraphDataParallel) on one GPU: an RCCL process group
-of world size 1 (the all-reduce runs, as an identity) — gradients land in the flat buffer, the
-eager step equals plain training bitwise, and the whole step including the RCCL all-reduce is
-captured and replayed as one HIP graph with the same parameter trajectory.
+"""Graph-captured data parallelism (sqr.dist.GraphDataParallel) on one GPU, on a world-1 RCCL
+communicator owned by libsqr (sqr.dist.Comm / sqr_comm_*): the all-reduce runs, as an identity.
+Gradients land in the flat buffer, the eager step equals plain training bitwise, the whole step
+including the RCCL all-reduce is captured and replayed as one HIP graph with the same parameter
+trajectory, train.py's CapturedStep survives partial batches (eager all-reduces between replays) and a
+learning-rate recapture, and train.py --dp-rehearsal matches the plain run.
 
 The checks run in a child process (tests/_dp_graph_child.py) that ends with the product teardown
-(sqr.dist.finish: the step graph destroyed before the RCCL communicator, host barrier, then
-destroy_process_group) and a normal exit: the test requires both markers and exit status 0, so an
-abort anywhere in the teardown or at interpreter exit fails it (in round 2 an eager RCCL barrier
-after CUDAGraph.reset() aborted; host-side synchronisation now runs on a gloo group)."""
+(sqr.dist.finish) and a normal exit: the test requires every marker and exit status 0, so an abort
+anywhere — including from a host thread polling captured work, the round-3 failure of the
+ProcessGroupNCCL-based design — fails it."""
 import os
 import subprocess
 import sys
@@ -22,7 +23,9 @@ def test_graph_dp_world1(tmp_path):
     env = dict(os.environ, NCCL_DEBUG="WARN")  # any RCCL complaint lands in the failure message
     r = subprocess.run([sys.executable, "-u", child, str(tmp_path)], capture_output=True, text=True, timeout=300,
                        env=env)
-    ok = r.returncode == 0 and "DP_GRAPH_OK" in r.stdout and "DP_TEARDOWN_OK" in r.stdout
+    marks = ("DP_GRAPH_OK", "DP_STEPPER_OK", "DP_TRAIN_OK", "DP_TEARDOWN_OK")
+    ok = r.returncode == 0 and all(m in r.stdout for m in marks)
+    key = []
     if not ok:
         # the error text first (a watchdog exception's what() line), then the raw streams in full
         key = [ln for ln in (r.stdout + r.stderr).splitlines()
