@@ -169,7 +169,7 @@ int sqr_conv2d_fwd(const void* x, const void* w_krsc, void* y, const sqr_conv_de
  * sqr_stem_fwd_stats so the BatchNorm that follows the conv never re-reads the activation. */
 size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
 /* Routing of bf16 3x3/stride-1/pad-1 forward and backward-data convs to the direct halo-window
- * kernels (C = K = 64, W = 64: the persistent resident-weight kernel; otherwise the tiled one),
+ * kernels (C = K = 64, W = 64 or 128: the persistent resident-weight kernel; otherwise the tiled one),
  * and of bf16 3x3/stride-2/pad-1 backward-data convs of ResNetSQ's layer 2-4 shapes to the direct
  * parity-class kernel: 1 (default) when the shape tiles and the grid fills the chip (stride 2:
  * whenever it tiles), 2 whenever the shape tiles, 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.

@@ -489,23 +489,27 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 
 
 // ============================================================================ layer-1 persistent
-// Cin = Nout = 64, W = 64 (ResNetSQ layer1, forward and backward-data).  One workgroup per band of
-// consecutive 2-row tiles of one image (B = 64: a quarter image = 8 tiles per workgroup):
+// Cin = Nout = 64, W = TW = 64 (ResNetSQ layer1 at 256x256 input; TH = 2-row tiles) or 128 (at
+// 512x512 input, config 5; 1-row tiles), forward and backward-data.  One workgroup per band of
+// consecutive TH-row tiles of one image (B = 64: a quarter image = 8 tiles at 64 x 64, 32 tiles at
+// 128 x 128 per workgroup):
 //  * each wave's share of the 3x3 weights (its 32 output channels x 576, 36 MFMA fragments) is
 //    loaded once (through a coalesced LDS image in the prologue) and held in VGPRs;
-//  * input rows live in an 8-slot LDS ring (slot = (row + 1) & 7; one image row + its 2 zero halo
-//    columns per slot): a tile reads 4 rows of which only 2 are new; the new rows of tile k+2 are
-//    loaded into registers during tile k's MFMA loop and written to the ring at the end of tile
-//    k+1, so every input row is fetched once per band;
-//  * the output tile is staged in LDS and written with 16-B coalesced stores during the next
-//    tile's MFMA loop; BatchNorm partials accumulate in registers, one partial row per workgroup.
+//  * input rows live in an NSLOT-slot LDS ring (slot = (row + 1) % NSLOT; one image row + its 2 zero
+//    halo columns per slot): a tile reads TH + 2 rows of which only TH are new; the new rows of tile
+//    k+2 are loaded into registers during tile k's MFMA loop and written to the ring at the end of
+//    tile k+1, so every input row is fetched once per band;
+//  * the output tile is staged in LDS (in the prologue's weight-image region, free once the weights
+//    are in registers) and written with 16-B coalesced stores during the next tile's MFMA loop;
+//    BatchNorm partials accumulate in registers, one partial row per workgroup.
+// A wave covers TH * TW / 2 consecutive pixels of the tile (2 x 2 waves: pixel half x channel half).
 struct D3PArgs {
-  const void* x;   // [N][H][64][64]
+  const void* x;   // [N][H][TW][64]
   const void* w;   // [64][9][64]
-  void* out;       // [N][H][64][64]
+  void* out;       // [N][H][TW][64]
   const void* addend;  // ACC launches: out = conv + addend (backward-data of a block input; may alias out)
   const uint8_t* addend_mask;  // nullable (ACC): the addend counts only where its bit is set
-  const void* bn_x;        // BNB launches: the following BatchNorm's input x [N][H][64][64] ...
+  const void* bn_x;        // BNB launches: the following BatchNorm's input x [N][H][TW][64] ...
   const uint8_t* bn_mask;  // ... its ReLU mask (1 bit / element) and ...
   const float* bn_mean;    // ... its batch mean: out = dgrad * mask, stats = its backward sums
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
@@ -524,27 +528,30 @@ struct D3PArgs {
 // stored value is g = dgrad * [relu mask] and a.stats receives, per workgroup, the BatchNorm
 // backward sums (sum g, sum g*(x - mean)) — what sqr_bn_bwd's separate reduction pass would read
 // back.  x and the mask of tile k are prefetched like ACC's addend.
-template <typename T, bool STATS, bool ACC = false, bool BNB = false>
+template <typename T, bool STATS, bool ACC = false, bool BNB = false, int TW = 64, int TH = 2>
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
-  constexpr int TW = 64, TH = 2, C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
-  // 2 x 2 waves, each 64 pixels (one image row) x 32 channels = two 32x32 MFMA accumulators
+  constexpr int C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
+  // 2 x 2 waves, each WM pixels x 32 channels = TM 32x32 MFMA accumulators
   // (v_mfma_f32_32x32x16_bf16: half the MFMA instructions of 16x16x32 for the same work, which
   // leaves the single wave per SIMD issue slots for its LDS reads)
-  constexpr int WAVES_M = 2, WAVES_N = 2, WM = 64, WN = 32, TM = WM / 32;
-  constexpr int SLOTR = 72;              // LDS rows per ring slot: 64 pixels + 2 halo, padded to 9 pieces
-  constexpr int PPR = SLOTR / 8;         // LDS-DMA pieces (8 rows = 1 KiB) per image row
-  constexpr int NSLOT = 8;
-  constexpr int RING = NSLOT * SLOTR * ROWB;  // 72 KiB
-  constexpr int WB = 9 * BN * ROWB;           // 72 KiB: prologue weight image, LDS row (tap, n)
-  constexpr int WPW = 9 * BN / (8 * NW);      // 18 weight pieces per wave
-  constexpr int STG = TH * TW * BN * 2;       // 16 KiB staged output tile
-  constexpr int NST = STG / 16 / NT;          // 16-B stores per thread per tile
-  static_assert(WM == TW && TM * 32 == WM && WN == 32, "a wave's pixels are one image row");
-  static_assert(2 * WAVES_M * 32 * BN * 4 <= RING, "statistics scratch fits the ring");
-  __shared__ __attribute__((aligned(1024))) char smem[WB + RING + STG];  // 160 KiB
-  char* const wl = smem + RING + STG;
+  constexpr int WAVES_M = 2, WAVES_N = 2, WM = TH * TW / WAVES_M, WN = 32, TM = WM / 32;
+  constexpr int SLOTR = (TW + 2 + 7) / 8 * 8;  // LDS rows per ring slot: TW pixels + 2 halo, whole pieces
+  constexpr int PPR = SLOTR / 8;               // LDS-DMA pieces (8 rows = 1 KiB) per image row
+  constexpr int NSLOT = TH + 2 <= 4 ? 4 : 8;   // the tile's TH + 2 rows; the next tile's new rows
+                                               // replace its first TH
+  constexpr int RING = NSLOT * SLOTR * ROWB;   // 36 KiB (TW 64) / 68 KiB (TW 128)
+  constexpr int WB = 9 * BN * ROWB;            // 72 KiB: prologue weight image, LDS row (tap, n)
+  constexpr int WPW = 9 * BN / (8 * NW);       // 18 weight pieces per wave
+  constexpr int STG = TH * TW * BN * 2;        // 16 KiB staged output tile (in the weight image's region)
+  constexpr int NST = STG / 16 / NT;           // 16-B stores per thread per tile
+  static_assert(TW % 32 == 0 && TM * 32 == WM && WN == 32, "a wave's pixels are whole 32-pixel runs of rows");
+  static_assert(STG <= WB, "the staged tile fits the weight image's region");
+  static_assert(2 * WAVES_M * 32 * BN * 4 <= RING && NT * 16 * 4 <= RING, "statistics scratch fits the ring");
+  static_assert(NST <= 8, "store schedule");
+  __shared__ __attribute__((aligned(1024))) char smem[WB + RING];  // 108 / 140 KiB
+  char* const wl = smem + RING;
   char* const ring = smem;
-  char* const stg = ring + RING;
+  char* const stg = wl;
   clock_begin(a.tp);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -566,7 +573,8 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // L%8, and the XOR swizzle is applied on the source side.
   // Input rows r0 .. r0+nrows-1 (row -1 / H: zero padding via the buffer range check); piece p
   // (8 LDS rows of one image row) belongs to wave p % 4.
-  constexpr int RPW = (2 * PPR + NW - 1) / NW;  // row pieces per wave for 2 rows (5)
+  constexpr int RPW = (TH * PPR + NW - 1) / NW;  // row pieces per wave for a tile's TH new rows (5)
+  constexpr int PRW = ((TH + 2) * PPR + NW - 1) / NW;  // ... for the TH + 2 rows of the first tile
   // (use = false: every lane's offset is out of range -- no memory access, and the instruction count
   // stays the same on every path, so the compiler's vmcnt waits stay exact)
   auto row_piece = [&](int r0, int p, uint32_t* vo, bool use = true) {  // -> LDS byte offset of this lane's 16 B
@@ -580,7 +588,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   };
   auto load_rows = [&](int r0, int nrows, u32x4* v, bool use) {  // every wave issues the same count
 #pragma unroll
-    for (int i = 0; i < (4 * PPR + NW - 1) / NW; ++i) {
+    for (int i = 0; i < PRW; ++i) {
       const int p = i * NW + wave;
       if (i < (nrows * PPR + NW - 1) / NW) {  // compile-time
         uint32_t vo;
@@ -589,15 +597,15 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       }
     }
   };
-  auto load_row_piece = [&](int r0, int i, u32x4* v, bool use) {  // piece i of 2 rows (RPW per wave)
+  auto load_row_piece = [&](int r0, int i, u32x4* v, bool use) {  // piece i of TH rows (RPW per wave)
     const int p = i * NW + wave;
     uint32_t vo;
-    row_piece(r0, p, &vo, use && p < 2 * PPR);
+    row_piece(r0, p, &vo, use && p < TH * PPR);
     v[i] = __builtin_amdgcn_raw_buffer_load_b128(xsrd, vo, 0, 0);
   };
   auto write_rows = [&](int r0, int nrows, const u32x4* v) {
 #pragma unroll
-    for (int i = 0; i < (4 * PPR + NW - 1) / NW; ++i) {
+    for (int i = 0; i < PRW; ++i) {
       const int p = i * NW + wave;
       if (i * NW + NW <= nrows * PPR || p < nrows * PPR) {
         uint32_t vo;
@@ -681,8 +689,8 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // end of tile t-1 (about 1.5 tiles of load latency hidden)
   u32x4 rvb[2][RPW];
   {
-    u32x4 t0[(4 * PPR + NW - 1) / NW], wv[WPW];
-    load_rows(hb - 1, 4, t0, true);  // tile 0: rows hb-1 .. hb+2
+    u32x4 t0[PRW], wv[WPW];
+    load_rows(hb - 1, TH + 2, t0, true);  // tile 0: rows hb-1 .. hb+TH
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {  // weight image: LDS row r = tap * 64 + n  <-  w[n][tap][0..63]
       const int r = (i * NW + wave) * 8 + prow;
@@ -690,14 +698,14 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       wv[i] = __builtin_amdgcn_raw_buffer_load_b128(
           wsrd, (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4)), 0, 0);
     }
-    write_rows(hb - 1, 4, t0);
+    write_rows(hb - 1, TH + 2, t0);
 #pragma unroll
     for (int i = 0; i < WPW; ++i) *(u32x4*)(wl + ((i * NW + wave) * 8) * ROWB + lane * 16) = wv[i];
   }
   // tile 1's new rows (written during tile 0).  Row loads are always the last vector-memory
   // instructions before the loop head, so the compiler's vmcnt waits for them are exact on both
   // paths into the loop (a younger store would make it wait for the store as well)
-  load_rows(hb + 3, 2, rvb[1], ntile > 1);
+  load_rows(hb + TH + 1, TH, rvb[1], ntile > 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   {
@@ -710,8 +718,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // One tile = 36 MFMA steps.  Its vector-memory work is spread over those steps instead of issued
   // in bursts at the tile boundary (every workgroup runs in lock-step with the others, so bursts
   // leave HBM idle during the MFMA loops and saturated in between: the kernel without its MFMA loop
-  // takes 11-13 us, with it 23-27 us): the 4 staged stores of tile k-1 at steps 1 + 8q, the row
-  // loads of tile k+2 at steps 3 + 7i, the addend / BatchNorm-input loads of tile k at 5 + 8q.
+  // takes 11-13 us, with it 23-27 us): the NST (4) staged stores of tile k-1 at steps 1 + 8q, the
+  // row loads of tile k+2 at steps 3 + 7i, the addend / BatchNorm-input loads of tile k at 5 + 8q.
+  constexpr int SSP = 32 / NST, RSP = 35 / RPW;
   auto tile = [&](int k, auto par) {
     constexpr int P = decltype(par)::value;  // k & 1 (static: selects the row buffers)
     f32x16 acc[TM];
@@ -719,18 +728,19 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-    // tap (r, c3) of output row hb+2k+wm reads input row hb+2k+wm+r-1 = ring slot (hb+2k+wm+r) & 7
-    const int rbase = hb + 2 * k + wm;
+    // tap (r, c3) of tile pixel (y, x) reads input row hb+TH*k+y+r-1 = ring slot (hb+TH*k+y+r) % NSLOT,
+    // LDS row x + c3 of it
+    const int rbase = hb + TH * k;
     // 36 (tap, 16-channel slice) steps; slice kk of a 128-B row = 16-B slots 2kk + h
     auto load = [&](int s, V8<T>* qf) {
       const int t = s >> 2, kk = s & 3;
       const int r = t / 3, c3 = t % 3;
       const int rr = flip ? 2 - r : r, cc = flip ? 2 - c3 : c3;
       const int slot = 2 * kk + h;
-      const int lrow0 = ((rbase + rr) & (NSLOT - 1)) * SLOTR + cc + r32;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int L = lrow0 + 32 * i;
+        const int m0 = wm * WM + 32 * i;  // the 32-pixel run's first tile pixel (wave-uniform)
+        const int L = ((rbase + m0 / TW + rr) & (NSLOT - 1)) * SLOTR + cc + (m0 % TW) + r32;
         qf[i] = *(const V8<T>*)(ring + L * ROWB + ((slot ^ ((L >> 1) & 7)) << 4));
       }
     };
@@ -740,11 +750,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     for (int s = 0; s < PD; ++s) load(s, qf[s]);
 #pragma unroll
     for (int s = 0; s < NSTEP; ++s) {
-      if (s % 8 == 1 && s / 8 < NST) store_piece(k - 1, k >= 1, s / 8);
-      if (s % 7 == 3 && s / 7 < RPW)
-        load_row_piece(hb + 2 * (k + 2) + 1, s / 7, rvb[P], k + 2 < ntile);
+      if (s % SSP == 1 && s / SSP < NST) store_piece(k - 1, k >= 1, s / SSP);
+      if (s % RSP == 3 % RSP && s / RSP < RPW)
+        load_row_piece(hb + TH * (k + 2) + 1, s / RSP, rvb[P], k + 2 < ntile);
       if constexpr (ACC || BNB)
-        if (s % 8 == 5 && s / 8 < NST) load_addend_piece(k, s / 8);
+        if (s % SSP == 5 % SSP && s / SSP < NST) load_addend_piece(k, s / SSP);
       if (s + PD < NSTEP) load(s + PD, qf[(s + PD) % (PD + 1)]);
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[i] = mfma32(wreg[s], qf[s % (PD + 1)][i], acc[i]);
@@ -797,8 +807,8 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         *(u32x2*)(stg + m * ROWB + ((((n >> 3) ^ key) << 4) | ((n & 7) << 1))) = u32x2{pk[i][g][0], pk[i][g][1]};
       }
     }
-    // tile k+1's new rows (loaded during tile k-1) into the slots of tile k-3's rows
-    if (k + 1 < ntile) write_rows(hb + 2 * (k + 1) + 1, 2, rvb[1 - P]);
+    // tile k+1's new rows (loaded during tile k-1) into the slots of tile k's first TH rows
+    if (k + 1 < ntile) write_rows(hb + TH * (k + 1) + 1, TH, rvb[1 - P]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // staged tile and tile k+1's rows visible
   };
@@ -1490,6 +1500,7 @@ struct D3Cfg {
 int g_direct = 1;  // 0 off, 1 on when the grid is big enough, 2 whenever the shape fits
 int g_persist = 1;  // layer-1 persistent kernel (0: the tiled conv3_kernel; tests compare the two)
 
+
 int pow2_log(int x) {
   int l = 0;
   while ((1 << l) < x) ++l;
@@ -1672,7 +1683,12 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   if (Cin % 64 || Nout % 64 || pow2_log(W) < 0) return kNotHandled;
   const size_t xbytes = (size_t)N * H * W * Cin * 2, wbytes = (size_t)Nout * 9 * Cin * 2;
   if (xbytes >= (1u << 31) || wbytes >= (1u << 31) || (size_t)N * H * W * Nout * 2 >= (1u << 31)) return kNotHandled;
-  if (Cin == 64 && Nout == 64 && W == 64 && H % 2 == 0 && g_persist) {
+  // the persistent kernel: 64-wide maps in 2-row tiles, 128-wide maps (512x512 input) in 1-row tiles
+  // (measured at B=64, 128 x 128, rocprof-free clock probe: fwd+stats 140 -> 101 us, dgrad 112 -> 91,
+  // dgrad+addend 146 -> 116 against the tiled kernel; 64-wide maps in 4-row tiles were slower than
+  // 2-row ones: fwd 31.5 vs 30.8 us, dgrad+addend 31.7 vs 29.0)
+  const int pth = W == 64 ? 2 : 1;  // rows per tile
+  if (Cin == 64 && Nout == 64 && (W == 64 || W == 128) && H % pth == 0 && g_persist) {
     static int ncu = 0;
     if (!ncu) {
       int dev = 0;
@@ -1680,7 +1696,7 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
       if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
     }
     // bands: the largest divisor of the per-image tile count giving about one workgroup per CU
-    const int tpi = H / 2;
+    const int tpi = H / pth;
     int bpi = 1;
     for (int d = 1; d <= tpi; ++d)
       if (tpi % d == 0 && (long long)N * d <= ncu) bpi = d;
@@ -1704,16 +1720,23 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     const int grid = N * bpi;
     if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
     probe_begin(st);
+#define SQR_D3P_LAUNCH(TW_, TH_)                                                                      \
+  if (bnb)                                                                                           \
+    hipLaunchKernelGGL((conv3p_kernel<T, false, false, true, TW_, TH_>), dim3(grid), dim3(256), 0, st, p); \
+  else if (stats)                                                                                    \
+    hipLaunchKernelGGL((conv3p_kernel<T, true, false, false, TW_, TH_>), dim3(grid), dim3(256), 0, st, p); \
+  else if (addend)                                                                                   \
+    hipLaunchKernelGGL((conv3p_kernel<T, false, true, false, TW_, TH_>), dim3(grid), dim3(256), 0, st, p); \
+  else                                                                                               \
+    hipLaunchKernelGGL((conv3p_kernel<T, false, false, false, TW_, TH_>), dim3(grid), dim3(256), 0, st, p);
     SQR_DISPATCH16(dtype, T, {
-      if (bnb)
-        hipLaunchKernelGGL((conv3p_kernel<T, false, false, true>), dim3(grid), dim3(256), 0, st, p);
-      else if (stats)
-        hipLaunchKernelGGL((conv3p_kernel<T, true>), dim3(grid), dim3(256), 0, st, p);
-      else if (addend)
-        hipLaunchKernelGGL((conv3p_kernel<T, false, true>), dim3(grid), dim3(256), 0, st, p);
-      else
-        hipLaunchKernelGGL((conv3p_kernel<T, false>), dim3(grid), dim3(256), 0, st, p);
+      if (W == 128) {
+        SQR_D3P_LAUNCH(128, 1)
+      } else {
+        SQR_D3P_LAUNCH(64, 2)
+      }
     });
+#undef SQR_D3P_LAUNCH
     probe_end(st);
     SQR_HIP_LAUNCH_CHECK("conv3p_kernel");
     return 0;

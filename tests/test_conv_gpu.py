@@ -181,18 +181,19 @@ def test_conv3_direct(shape, dtype):
     assert _rel(res[2][3], res[0][3]) <= 2e-4
 
 
-@pytest.mark.parametrize("N", [64, 48, 128])
-def test_conv3_persistent_bands(N):
-    """The layer-1 persistent kernel at benchmark-sized batches (bands of 8 and 16 tiles per
-    workgroup, the 8-slot row ring wrapping several times) against the implicit-GEMM kernel on the
-    same bf16 inputs, plus its per-workgroup BatchNorm partials against the output itself."""
+@pytest.mark.parametrize("N,H", [(64, 64), (48, 64), (128, 64), (64, 128), (48, 128), (16, 128)])
+def test_conv3_persistent_bands(N, H):
+    """The layer-1 persistent kernel at benchmark-sized batches (64 x 64 maps in 2-row tiles: bands
+    of 8 and 16 tiles per workgroup; 128 x 128 maps, config 5, in 1-row tiles: bands of 32 / 8; the
+    row ring wrapping many times) against the implicit-GEMM kernel on the same bf16 inputs, plus its
+    per-workgroup BatchNorm partials against the output itself."""
     from sqr import conv as sc
     from sqr._lib import lib
-    g = torch.Generator(device=DEV).manual_seed(N)
-    x = torch.randn(N, 64, 64, 64, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    g = torch.Generator(device=DEV).manual_seed(N + H)
+    x = torch.randn(N, 64, H, H, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
     w = torch.randn(64, 64, 3, 3, device=DEV, generator=g) / 24.0
-    gy = torch.randn(N, 64, 64, 64, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
-    d = sc._desc(N, 64, 64, 64, 64, 3, 3, 1, 1, torch.bfloat16)
+    gy = torch.randn(N, 64, H, H, device=DEV, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    d = sc._desc(N, 64, H, H, 64, 3, 3, 1, 1, torch.bfloat16)
     krsc, crsk = sc.pack_weight(w, d, True)
     res = {}
     old = lib().sqr_conv_set_direct(1)
@@ -262,18 +263,19 @@ def _f64_fwd_dgrad_wgrad(x, w, gy, stride, pad):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
-@pytest.mark.parametrize("N", [64, 48])
-def test_conv3p_bench_size_vs_f64(N, dtype):
-    """Layer-1 3x3 64->64 at the bench batch: the persistent resident-weight kernel (bands of 8+
-    tiles per workgroup, the row ring wrapping) for forward and backward-data, the direct weight
-    gradient, and the fused BatchNorm partials — all against float64."""
+@pytest.mark.parametrize("N,H", [(64, 64), (48, 64), (16, 128)])
+def test_conv3p_bench_size_vs_f64(N, H, dtype):
+    """Layer-1 3x3 64->64 at the bench batch (config 5's 128 x 128 maps at batch 16): the
+    persistent resident-weight kernel (bands of 8+ tiles per workgroup, the row ring wrapping) for
+    forward and backward-data, the direct weight gradient, and the fused BatchNorm partials — all
+    against float64."""
     from sqr import conv as sc
-    g = torch.Generator().manual_seed(1000 + N)
-    x = torch.randn(N, 64, 64, 64, generator=g).to(dtype).float()
+    g = torch.Generator().manual_seed(1000 + N + H)
+    x = torch.randn(N, 64, H, H, generator=g).to(dtype).float()
     w = (torch.randn(64, 64, 3, 3, generator=g) / 24.0)
-    gy = torch.randn(N, 64, 64, 64, generator=g).to(dtype).float()
+    gy = torch.randn(N, 64, H, H, generator=g).to(dtype).float()
     yr, dxr, dwr = _f64_fwd_dgrad_wgrad(x, w.to(dtype).float(), gy, 1, 1)
-    d = sc._desc(N, 64, 64, 64, 64, 3, 3, 1, 1, dtype)
+    d = sc._desc(N, 64, H, H, 64, 3, 3, 1, 1, dtype)
     krsc, crsk = sc.pack_weight(w.to(DEV), d, True)
     xg = x.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
     gyg = gy.to(DEV).to(dtype).contiguous(memory_format=torch.channels_last)
@@ -445,7 +447,7 @@ ACC_SHAPES = [
     (4, 64, 64, 64, 3, 1), (64, 64, 64, 64, 3, 1), (48, 64, 64, 64, 3, 1),
     (4, 128, 32, 128, 3, 1), (4, 256, 16, 256, 3, 1), (4, 512, 8, 512, 3, 1),
     (4, 64, 64, 128, 3, 2), (4, 128, 32, 256, 3, 2), (4, 256, 16, 512, 3, 2), (64, 64, 64, 128, 3, 2),
-    (4, 64, 64, 128, 1, 2), (2, 64, 128, 64, 3, 1), (2, 64, 128, 128, 3, 2),
+    (4, 64, 64, 128, 1, 2), (2, 64, 128, 64, 3, 1), (2, 64, 128, 128, 3, 2), (16, 64, 128, 64, 3, 1),
     # 512x512 input at batch 16 (config 5's step test): several tiles per image row in the tiled
     # 8-wave layer-2 kernel and the layer-3 stride-2 kernel
     (16, 128, 64, 128, 3, 1), (16, 128, 64, 256, 3, 2), (16, 256, 32, 512, 3, 2), (16, 256, 32, 256, 3, 1),
@@ -485,7 +487,7 @@ def test_conv_bwd_data_acc(shape, dtype):
 # (dy, mask) (sqr.conv.MaskedGrad); must equal the ACC launch on the materialised masked tensor
 # bitwise (masked-out halves are +0 either way), and float64 within the 16-bit tolerance.
 MASKED_SHAPES = [(4, 64, 64, 64), (64, 64, 64, 64), (4, 128, 32, 128), (4, 256, 16, 256), (4, 512, 8, 512),
-                 (64, 128, 32, 128), (64, 512, 8, 512)]
+                 (64, 128, 32, 128), (64, 512, 8, 512), (16, 64, 128, 64)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
@@ -563,7 +565,8 @@ def test_conv_bwd_data_acc_s2(shape, dtype):
 
 
 BNB_SHAPES = [(4, 64, 64, 64), (64, 64, 64, 64), (4, 128, 32, 128), (64, 128, 32, 128), (4, 256, 16, 256),
-              (4, 512, 8, 512), (2, 64, 128, 64), (3, 32, 20, 32), (16, 128, 64, 128), (16, 256, 32, 256)]
+              (4, 512, 8, 512), (2, 64, 128, 64), (3, 32, 20, 32), (16, 128, 64, 128), (16, 256, 32, 256),
+              (16, 64, 128, 64)]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32], ids=["bf16", "f16", "f32"])
