@@ -257,18 +257,40 @@ def time_loss_call(crit, images, B, dev, reps=20):
 _PROBE_RE = r"conv3p_kernel(IDF16b?Lb1E|<[^<>]*?,\s*true,|<bool _Accum, bool, E, false, false>)"
 
 
+def kernel_src_sha():
+    """sha256 of the HIP / C++ sources of libsqr and its header (what a PMC summary was collected on)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "sq-recovery_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "sq-recovery_amd", "csrc", "*.h")) +
+                   glob.glob(os.path.join(ROOT, "sq-recovery_amd", "csrc", "*.cpp")) +
+                   [os.path.join(ROOT, "include", "sqr.h")])
+    for path in files:
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_summary(H, dname):
     """MFMA-busy and issue counters of the step's kernels from the committed rocprofv3 PMC summary
     (profiles/pmc_step.json, written by tools/pmc_step.py from tools/gpu_pmc_step.sh on the default
     config-2 step): the probe kernel's counters and the step-wide MFMA utilisation (MFMA-busy cycles of
-    every kernel over every kernel's duration x 1024 SIMDs)."""
+    every kernel over every kernel's duration x 1024 SIMDs).  Counters collected on other kernel
+    sources than the ones built here (src_sha) are not reported: only the staleness is."""
     import re
     path = os.path.join(ROOT, "profiles", "pmc_step.json")
     if not os.path.exists(path) or H != 256 or dname != "bf16":
         return None
     with open(path) as f:
-        rows = json.load(f)
-    out = {"source": "profiles/pmc_step.json (rocprofv3 --pmc, eager step, mean per dispatch)"}
+        data = json.load(f)
+    rows, sha = (data, None) if isinstance(data, list) else (data["rows"], data.get("src_sha"))
+    cur = kernel_src_sha()
+    if sha != cur:
+        return {"stale": True, "collected_src_sha": sha, "current_src_sha": cur,
+                "source": "profiles/pmc_step.json (collected on other kernel sources: counters omitted)"}
+    out = {"source": "profiles/pmc_step.json (rocprofv3 --pmc, eager step, mean per dispatch)", "src_sha": sha}
     probe = [r for r in rows if re.search(_PROBE_RE, r["kernel"])]
     if probe:
         r = probe[0]
@@ -487,10 +509,15 @@ def main():
             with open(path) as f:
                 trf = json.load(f)
             if trf.get("kernel_key") == list(PROBE) and H == 256 and dname == "bf16":
-                roof["traffic"] = trf.get("hbm_bytes_per_launch")
+                if trf.get("src_sha") == kernel_src_sha():
+                    roof["traffic"] = trf.get("hbm_bytes_per_launch")
+                else:  # measured on other kernel sources: not this build's traffic
+                    roof["traffic_stale"] = {"collected_src_sha": trf.get("src_sha"),
+                                             "hbm_bytes_per_launch": trf.get("hbm_bytes_per_launch")}
         pmc = pmc_summary(H, dname)
         if pmc:
-            roof["mfma_busy"] = pmc.get("probe", {}).get("mfma_busy")
+            if not pmc.get("stale"):
+                roof["mfma_busy"] = pmc.get("probe", {}).get("mfma_busy")
             roof["pmc"] = pmc
         out["roofline"] = roof
         # secondary rooflines: the whole step's conv work against the MFMA peak, and

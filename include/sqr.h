@@ -352,8 +352,15 @@ int sqr_stem_bwd(const void* dpool, const void* ypool, const uint8_t* argmax, co
 /* resnet18 stem of ResNetSQ (torch/models.py:181-184) for 16-bit training / inference:
  * y = maxpool3x3/s2/p1(relu(bn1(conv1(x)))), conv1 = 1 -> 64 channels, 7x7, stride 2, pad 3, no
  * bias, computed in y_dtype (bf16 or fp16; fp32 accumulation) WITHOUT materialising the conv1
- * activation: the forward recomputes conv1 for the BatchNorm statistics and for the pooling, the
- * backward recomputes it and forms dW / dgamma / dbeta in closed form (no input gradient).
+ * activation: the forward recomputes conv1 for the BatchNorm statistics and for the pooling.  The
+ * backward does not recompute conv1: per tile it accumulates, over the input patches A, the Gram
+ * matrix S = sum A A^T and T1 = sum g A (g = the pooled gradient routed to its argmax pixel), then
+ * T2 = W S and sum g*x = rowsum(W o T1) give dW / dgamma / dbeta in closed form (BatchNorm's
+ * backward is linear in g, x and 1; no input gradient).  Known deviation from torch: x in these
+ * sums is the f32 conv value, where torch's BatchNorm backward reads the 16-bit-rounded stored
+ * conv1 output; the difference is within the 16-bit rounding of x and is covered by the
+ * tolerance tests/test_step_gpu.py derives from a CPU float32 emulation that rounds at the GPU
+ * step's storage points (every parameter gradient within 3x of that emulation's error vs float64).
  *   x [N][H][W] (x_dtype f32, bf16 or fp16), w [64][1][7][7] f32, y [N][Hp][Wp][64] y_dtype (NHWC),
  *   argmax [N][Hp][Wp][64] u8 (window tap of the first maximum; written when training).
  * Shapes: the conv1 output (H/2 x W/2) must tile by 8 x 32 and the pooled one by 8 x 16

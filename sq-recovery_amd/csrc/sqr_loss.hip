@@ -11,14 +11,14 @@
 //   loss               classes.py:284-295 (nearest resize, mean |true - D|, mean over batch)
 //
 // MI355X design.  The grid is generated from the voxel index (no HBM reads), so the kernel is
-// bound by VALU transcendentals, not HBM: per voxel ~11 v_exp/v_log in the forward ray pass and
-// ~17 in the backward ray pass.  The pow chain is evaluated in the log2 domain
+// bound by VALU transcendentals, not HBM: per voxel ~11 v_exp/v_log for the forward chain and ~7
+// for its Jacobian.  The pow chain is evaluated in the log2 domain
 // (lA = log2(A1)/e2, log2(A+B) = max + log2(1 + 2^-|d|), ...) so nothing under/overflows in
 // fp32 where the reference's float64 does not, and every ratio the backward needs (A/F1, C/F/C1,
-// ...) is a single exp2 of a difference of logs.  One thread owns one ray (one output pixel):
-// pass 1 walks the ray top-down (flipped z, classes.py:277) accumulating S, T = exp(-tau S) into
-// LDS; pass 2 walks it bottom-up summing the suffix sums of T exactly (no cancellation) and
-// recomputes the voxel chain to push dL/docc back to 17 per-sample parameter moments.  Blocks
+// ...) is a single exp2 of a difference of logs.  One thread owns one ray (one output pixel) and
+// walks it once, top-down (flipped z, classes.py:277), accumulating S, T = exp(-tau S), the 17
+// per-sample parameter moments of each voxel's Jacobian and their prefix-of-T-weighted sums (the
+// suffix sums of T the gradient needs are Ttot - prefix: implicit_loss_kernel).  Blocks
 // reduce those moments with DPP wave sums + LDS and write per-block partials; a one-thread-per-
 // sample finalize kernel sums them in a fixed order (bitwise reproducible) in float64 and applies
 // the closed-form chain through u = Rc (g - t)/a, the quaternion and the clamp masks.
@@ -178,6 +178,16 @@ __device__ __forceinline__ void vox_bwd(const SQ& s, const Vox& f, float occ, fl
   M.m[16] = fmaf(gu2, gz, M.m[16]);
 }
 
+// dL/docc = 1 at one voxel: its 17 parameter moments J (vox_bwd is gocc * J)
+__device__ __forceinline__ void vox_jac(const SQ& s, const Vox& f, float occ, float omo, float sharp, float gx,
+                                        float gy, float gz, float* J) {
+  Moments M;
+  M.zero();
+  vox_bwd(s, f, occ, omo, 1.f, sharp, gx, gy, gz, M);
+#pragma unroll
+  for (int i = 0; i < 17; ++i) J[i] = M.m[i];
+}
+
 // block-wide sum of kNAcc floats -> out (thread 0..kNAcc-1 write)
 template <int NT>
 __device__ __forceinline__ void block_reduce_store(float* vals, float* red, float* out) {
@@ -197,8 +207,18 @@ __device__ __forceinline__ void block_reduce_store(float* vals, float* red, floa
 }
 
 // -------------------------------------------------------------------------- ImplicitLoss
-// grid: (blocks_per_sample, B); one thread per output pixel (ray).
-// dyn LDS: T[R][NT] floats (pass-2 suffix sums) + axis[R] + reduction scratch.
+// grid: (blocks_per_sample, B); one thread per output pixel (ray), walking it ONCE, top-down
+// (flipped z, classes.py:277).
+// Gradient: dL/docc_m = cg * sum_{k>=m} T_k (the suffix of the transmittances, cg = sign(D - true)
+// tau / R), and the 17 moments are linear in dL/docc: M = sum_m suffix_m J_m (J_m = voxel m's
+// moments at dL/docc = 1).  With suffix_m = Ttot - P_{m-1} (P the exclusive prefix of T),
+// M = cg (Ttot * sum J - sum P_{m-1} J_m): both sums accumulate on the way down, so the voxel chain
+// is evaluated once (round 3's second, bottom-up pass recomputed it for the suffix sums: 28 instead
+// of 18 transcendentals per voxel, T kept in LDS; B = 64 call 31 -> 27 us at R = 32, kernel 97 -> 85
+// us at R = 64).  The subtraction cancels where the suffix is small next to Ttot (behind the
+// surface, where J is small too): relative error ~ eps * Ttot / suffix.  (Splitting a ray over 4
+// lanes, segment transmittances combined by lane scans, measured slower: 32 / 121 us.)
+// dyn LDS: axis[R] + reduction scratch.
 template <int NT, bool NEED_GRAD>
 __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     const float* __restrict__ params, const float* __restrict__ target, int H, int W, int R,
@@ -206,7 +226,6 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
   extern __shared__ float lds[];
   float* axis = lds;                           // [R]
   float* red = axis + ((R + 3) & ~3);          // [NT/64][kNAcc]
-  float* Tbuf = red + (NT / 64) * kNAcc;       // [R][NT]
   const int b = blockIdx.y;
   const int nblk = gridDim.x;
   for (int i = threadIdx.x; i < R; i += NT)
@@ -225,8 +244,10 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     const int ix = c, iy = R - 1 - r;  // D[r,c] = depth[x=c, y=R-1-r] (classes.py:279)
     const float gx = axis[ix], gy = axis[iy];
     const float dx = gx - s.t[0], dy = gy - s.t[1];
-    // pass 1: top-down along z (flip, classes.py:277)
-    float S = 0.f, sumOM = 0.f;
+    float S = 0.f, P = 0.f;  // occupancy sum, prefix of T
+    float JA[NEED_GRAD ? 17 : 1], JB[NEED_GRAD ? 17 : 1];  // sum J, sum P_{m-1} J_m
+#pragma unroll
+    for (int i = 0; i < (NEED_GRAD ? 17 : 1); ++i) JA[i] = JB[i] = 0.f;
     const float ntau = -tau * kLog2e;
     for (int k = 0; k < R; ++k) {
       const float gz = axis[R - 1 - k];
@@ -236,10 +257,18 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
       occupancy(f.G, sharp, occ, omo);
       S += occ;
       const float T = fexp2(ntau * S);
-      sumOM += 1.f - T;
-      if (NEED_GRAD) Tbuf[k * NT + threadIdx.x] = T;
+      if (NEED_GRAD) {
+        float J[17];
+        vox_jac(s, f, occ, omo, sharp, gx, gy, gz, J);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) {
+          JA[i] += J[i];
+          JB[i] = fmaf(P, J[i], JB[i]);
+        }
+      }
+      P += T;
     }
-    const float D = sumOM / (float)R;  // 1 - sum(T)/R (classes.py:278)
+    const float D = 1.f - P / (float)R;  // 1 - sum(T)/R (classes.py:278)
     // F.interpolate nearest (float scale, floor, clamp)
     const float sh = (float)H / (float)R, sw = (float)W / (float)R;
     const int sr = min((int)floorf((float)r * sh), H - 1);
@@ -248,22 +277,10 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     const float diff = D - tv;
     vals[17] = fabsf(diff);
     if (NEED_GRAD && diff != 0.f) {
-      // dL/docc_m = sign(D-true) * tau/R * sum_{k>=m} T_k   (scaled by 1/(B R^2) in finalize)
+      // dL/docc_m = sign(D-true) * tau/R * (Ttot - P_{m-1})   (scaled by 1/(B R^2) in finalize)
       const float cg = (diff > 0.f ? 1.f : -1.f) * tau / (float)R;
-      Moments M;
-      M.zero();
-      float suffix = 0.f;
-      for (int k = R - 1; k >= 0; --k) {
-        suffix += Tbuf[k * NT + threadIdx.x];
-        const float gz = axis[R - 1 - k];
-        Vox f;
-        vox_fwd(s, dx, dy, gz - s.t[2], f);
-        float occ, omo;
-        occupancy(f.G, sharp, occ, omo);
-        vox_bwd(s, f, occ, omo, cg * suffix, sharp, gx, gy, gz, M);
-      }
 #pragma unroll
-      for (int i = 0; i < 17; ++i) vals[i] = M.m[i];
+      for (int i = 0; i < 17; ++i) vals[i] = cg * fmaf(P, JA[i], -JB[i]);
     }
   }
   block_reduce_store<NT>(vals, red, partials + ((size_t)b * nblk + blockIdx.x) * kNAcc);
@@ -531,9 +548,8 @@ using namespace sqr;
 // ============================================================================ C ABI
 static int implicit_threads(int R) { return R > 128 ? 128 : 256; }
 
-static size_t implicit_lds_bytes(int R, int NT, bool grad) {
-  size_t n = ((R + 3) & ~3) + (size_t)(NT / 64) * kNAcc;
-  if (grad) n += (size_t)R * NT;
+static size_t implicit_lds_bytes(int R, int NT, bool /*grad*/) {
+  const size_t n = ((R + 3) & ~3) + (size_t)(NT / 64) * kNAcc;
   return n * sizeof(float);
 }
 
@@ -565,21 +581,15 @@ extern "C" int sqr_implicit_loss_fwd_bwd_mean(const float* params, const float* 
   float* partials = (float*)workspace;
   const dim3 grid(nblk, B);
   const size_t lds = implicit_lds_bytes(R, NT, need_grad != 0);
-  if (NT == 256) {
-    if (need_grad)
-      hipLaunchKernelGGL((implicit_loss_kernel<256, true>), grid, dim3(256), lds, st, params, target, H, W,
-                         R, tau, sharpness, partials);
-    else
-      hipLaunchKernelGGL((implicit_loss_kernel<256, false>), grid, dim3(256), lds, st, params, target, H,
-                         W, R, tau, sharpness, partials);
-  } else {
-    if (need_grad)
-      hipLaunchKernelGGL((implicit_loss_kernel<128, true>), grid, dim3(128), lds, st, params, target, H, W,
-                         R, tau, sharpness, partials);
-    else
-      hipLaunchKernelGGL((implicit_loss_kernel<128, false>), grid, dim3(128), lds, st, params, target, H,
-                         W, R, tau, sharpness, partials);
-  }
+  // (the gradient moments are computed whether or not they are wanted: the kernel without them
+  // compiles the shared forward chain differently and its loss would differ in the last bits;
+  // ImplicitLoss's value must not depend on torch.no_grad)
+  if (NT == 256)
+    hipLaunchKernelGGL((implicit_loss_kernel<256, true>), grid, dim3(256), lds, st, params, target, H, W, R, tau,
+                       sharpness, partials);
+  else
+    hipLaunchKernelGGL((implicit_loss_kernel<128, true>), grid, dim3(128), lds, st, params, target, H, W, R, tau,
+                       sharpness, partials);
   SQR_HIP_LAUNCH_CHECK("implicit_loss_kernel");
   const double rr = (double)R * (double)R;
   launch_finalize(st, params, partials, B, nblk, 1.0 / rr, 1.0 / ((double)B * rr), need_grad, loss_per_sample,

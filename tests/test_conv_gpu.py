@@ -604,3 +604,4 @@ def test_conv_bwd_data_bn(shape, dtype):
     tot = st.double().sum(0).cpu()
     assert st.shape[1:] == (2, C)
     assert _rel(tot[0], s1) <= 1e-5 and _rel(tot[1], s2) <= 1e-5
+

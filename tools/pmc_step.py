@@ -101,6 +101,9 @@ for d in rows:
         "%.0f" % d["insts_valu"] if "insts_valu" in d else "-",
         "%.2f" % d["lds_conflict"] if "lds_conflict" in d else "-",
         "%.1f" % (d["hbm_bytes"] / 1e6) if "hbm_bytes" in d else "-"))
+# the kernel sources the counters were collected on (bench.py omits the counters once they change)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_src_sha  # noqa: E402
 out = os.path.join(ROOT, "pmc_step.json")
 with open(out, "w") as f:
-    json.dump(rows, f, indent=1)
+    json.dump({"src_sha": kernel_src_sha(), "rows": rows}, f, indent=1)

@@ -52,7 +52,10 @@ def main():
         pick = list(fetch)
     fv = [v for n in pick for v in fetch.get(n, [])]
     wv = [v for n in pick for v in write.get(n, [])]
-    res = {"kernel": kernel, "kernel_key": PROBE_KEY, "instances": pick, "dispatches": [len(fv), len(wv)]}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_src_sha
+    res = {"kernel": kernel, "kernel_key": PROBE_KEY, "src_sha": kernel_src_sha(), "instances": pick,
+           "dispatches": [len(fv), len(wv)]}
     if fv and wv:
         f = sum(fv) / len(fv) * 1024.0 * 2.0  # KiB -> B, gfx950 half-count correction
         w = sum(wv) / len(wv) * 1024.0
