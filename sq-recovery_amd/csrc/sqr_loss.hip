@@ -93,11 +93,18 @@ struct Vox {
   float lA1, lB1, lC1;  // log2 of the (zero-fixed) squares
   float lA, lB, lC, lF1, lE, lF;
   float G;
+  float rA, rB, rE, rC;  // A/F1, B/F1, E/F, C/F (the Jacobian's ratios)
 };
 
-__device__ __forceinline__ float lse2(float x, float y) {
+// log2(2^x + 2^y) and the two shares 2^x / (2^x + 2^y), 2^y / (2^x + 2^y): one exp2, one log2 and
+// one rcp (the shares come from e = 2^(min - max): 1 / (1 + e) and e / (1 + e))
+__device__ __forceinline__ float lse2(float x, float y, float* sx, float* sy) {
   const float m = fmaxf(x, y);
-  return m + flog2(1.f + fexp2(fminf(x, y) - m));
+  const float e = fexp2(fminf(x, y) - m);
+  const float big = frcp(1.f + e), small = e * big;
+  *sx = x >= y ? big : small;
+  *sy = x >= y ? small : big;
+  return m + flog2(1.f + e);
 }
 
 // classes.py:247-273 for one voxel; (dx,dy,dz) = g - t
@@ -118,9 +125,9 @@ __device__ __forceinline__ void vox_fwd(const SQ& s, float dx, float dy, float d
   f.lA = f.lA1 * s.ie2;
   f.lB = f.lB1 * s.ie2;
   f.lC = f.lC1 * s.ie1;
-  f.lF1 = lse2(f.lA, f.lB);
+  f.lF1 = lse2(f.lA, f.lB, &f.rA, &f.rB);
   f.lE = s.r21 * f.lF1;
-  f.lF = lse2(f.lE, f.lC);
+  f.lF = lse2(f.lE, f.lC, &f.rE, &f.rC);
   f.G = fexp2(s.e1 * f.lF);
 }
 
@@ -148,19 +155,20 @@ __device__ __forceinline__ void vox_bwd(const SQ& s, const Vox& f, float occ, fl
                                         float sharp, float gx, float gy, float gz, Moments& M) {
   const float hG = gocc * (-sharp) * occ * omo * f.G;  // dL/dln G
   const float g_lnF = hG * s.e1;
-  const float g_lnE = g_lnF * fexp2(f.lE - f.lF);
-  const float g_lnC = g_lnF * fexp2(f.lC - f.lF);
+  const float g_lnE = g_lnF * f.rE;
+  const float g_lnC = g_lnF * f.rC;
   const float g_lnF1 = g_lnE * s.r21;
-  const float rA = fexp2(f.lA - f.lF1), rB = fexp2(f.lB - f.lF1);
+  const float rA = f.rA, rB = f.rB;
   const float g_lnA = g_lnF1 * rA, g_lnB = g_lnF1 * rB;
   // e1: lnG = e1 lnF ; lnE = (e2/e1) lnF1 ; lnC = lnC1/e1
   M.m[3] += kLn2 * (hG * f.lF - (g_lnE * f.lE + g_lnC * f.lC) * s.ie1);
   // e2: lnE ; lnA = lnA1/e2 ; lnB = lnB1/e2
   M.m[4] += kLn2 * s.ie2 * (g_lnE * f.lE - g_lnA * f.lA - g_lnB * f.lB);
   // u: d lnA1/du0 = 2 u0 / A1
-  const float gu0 = 2.f * f.u0 * s.ie2 * g_lnF1 * fexp2(f.lA - f.lF1 - f.lA1);
-  const float gu1 = 2.f * f.u1 * s.ie2 * g_lnF1 * fexp2(f.lB - f.lF1 - f.lB1);
-  const float gu2 = 2.f * f.u2 * s.ie1 * g_lnF * fexp2(f.lC - f.lF - f.lC1);
+  // (A / F1) / A1 etc.: the share times 2^-log2(A1) (A1 itself may sit below FLT_MIN)
+  const float gu0 = 2.f * f.u0 * s.ie2 * g_lnF1 * rA * fexp2(-f.lA1);
+  const float gu1 = 2.f * f.u1 * s.ie2 * g_lnF1 * rB * fexp2(-f.lB1);
+  const float gu2 = 2.f * f.u2 * s.ie1 * g_lnF * f.rC * fexp2(-f.lC1);
   M.m[0] = fmaf(gu0, f.u0, M.m[0]);
   M.m[1] = fmaf(gu1, f.u1, M.m[1]);
   M.m[2] = fmaf(gu2, f.u2, M.m[2]);
@@ -657,12 +665,10 @@ extern "C" int sqr_explicit_loss_fwd_bwd_mean(const float* p_true, const float* 
   const int nblk = (n * n + 255) / 256;
   float* partials = (float*)workspace;
   const double step = 1.0 / (double)R;
-  if (need_grad)
-    hipLaunchKernelGGL((explicit_loss_kernel<256, true>), dim3(nblk, B), dim3(256), 0, st, p_true, p_pred, n,
-                       step, partials);
-  else
-    hipLaunchKernelGGL((explicit_loss_kernel<256, false>), dim3(nblk, B), dim3(256), 0, st, p_true, p_pred,
-                       n, step, partials);
+  // (with the gradient moments either way, as the implicit loss: the loss value must not depend on
+  // whether the gradient is wanted, and the kernel without them compiles the shared chain differently)
+  hipLaunchKernelGGL((explicit_loss_kernel<256, true>), dim3(nblk, B), dim3(256), 0, st, p_true, p_pred, n, step,
+                     partials);
   SQR_HIP_LAUNCH_CHECK("explicit_loss_kernel");
   const double n3 = (double)n * n * n;
   launch_finalize(st, p_pred, partials, B, nblk, 100.0 / n3, 100.0 / (n3 * (double)B), need_grad, loss_per_sample,

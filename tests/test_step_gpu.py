@@ -8,9 +8,11 @@ step on the same images and the same 16-bit-rounded conv weights.  The tolerance
 guessed: a CPU float32 run that rounds to the compute dtype at the GPU step's storage points (conv
 operands and outputs, BatchNorm / pooled activations, and - through autograd of the casts - the
 activation gradients) measures how far a correct 16-bit step lands from float64; the GPU step must
-land as close (L2 error x3, max error x5, with a small absolute floor for parameters whose
-gradient is ~0).
+land as close (L2 error x4 per parameter and x1.6 as the geometric mean over all parameters, max
+error x5, with a small absolute floor for parameters whose gradient is ~0).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -91,7 +93,8 @@ def _fix_tail(model, masks):
 def test_bench_step_gradients_vs_f64(config, batch, dtype):
     import bench
     import ref_torch
-    tr = bench.Trainer(torch.device(DEV), config=config, batch=batch, dtype=dtype)
+    seed = int(os.environ.get("SQR_STEP_SEED", "1234"))  # data seed (rehearsals of the error statistics)
+    tr = bench.Trainer(torch.device(DEV), config=config, batch=batch, dtype=dtype, seed=seed)
     dt = tr.dtype
     tr.capture()
     assert tr.graph is not None
@@ -131,20 +134,30 @@ def test_bench_step_gradients_vs_f64(config, batch, dtype):
         h.remove()
 
     assert abs(loss_gpu - loss64) <= max(3 * abs(loss_emu - loss64), 1e-4 * abs(loss64)), (loss_gpu, loss_emu, loss64)
-    # Two error measures per parameter, each against the emulation's: the L2-relative error (x3) and
-    # the max-abs relative error (x5).  A ReLU input within rounding distance of 0 takes either
-    # branch in a correct 16-bit step; one such element moves one channel of a BatchNorm gradient,
-    # so the per-channel maximum is heavy-tailed (measured: cfg5 fp16 B=16 layer4.0.bn1.bias max
-    # ratio 3.7 with L2 ratio 1.1) while the L2 error of a correct step stays within ~2.5x.
-    worst = []
+    # Two error measures per parameter, each against the emulation's: the L2-relative error and the
+    # max-abs relative error (x5), plus the geometric mean of the L2 ratios over all parameters
+    # (<= 1.6: a systematic error moves many parameters at once, noise does not).  A ReLU input
+    # within rounding distance of 0 takes either branch in a correct 16-bit step; one such element
+    # moves one channel of a BatchNorm gradient, so the per-channel maximum is heavy-tailed
+    # (measured: cfg5 fp16 B=16 layer4.0.bn1.bias max ratio 3.7 with L2 ratio 1.1).  The per-
+    # parameter L2 ratio of a correct step is heavy-tailed too at bf16 with 16 images: the head
+    # biases' gradients are sums over 16 predictions, each a chaotic function of the bf16 forward
+    # (measured, cfg5 bf16 B=16, data seeds 1234/1/2/3, the tiled layer-1 kernel and the persistent
+    # one — each against float64 in tests/test_conv_gpu.py: worst ratios 1.2 / 1.6 / 2.2 / 1.2 and
+    # 3.4 / 2.1 / 1.8 / 1.5, output_rotation.out_layer.0.bias at 3.4), hence x4.
+    worst, logr = [], []
     for n, b in g64.items():
         e_gpu, e_emu = _rel_err(g_gpu[n], b), _rel_err(g_emu[n], b)
         l_gpu, l_emu = _l2_err(g_gpu[n], b), _l2_err(g_emu[n], b)
         worst.append((l_gpu / max(l_emu, 1e-4), n, l_gpu, l_emu, e_gpu, e_emu))
+        logr.append(np.log(max(l_gpu, 1e-4) / max(l_emu, 1e-4)))
     worst.sort(reverse=True)
-    print("worst gpu/emulated L2 (max) error:", ["%s %.2e/%.2e (%.2e/%.2e)" % w[1:] for w in worst[:8]])
+    gmean = float(np.exp(np.mean(logr)))
+    print("worst gpu/emulated L2 (max) error:", ["%s %.2e/%.2e (%.2e/%.2e)" % w[1:] for w in worst[:8]],
+          "geometric mean L2 ratio %.3f" % gmean)
+    assert gmean <= 1.6, gmean
     for _, n, l_gpu, l_emu, e_gpu, e_emu in worst:
-        assert l_gpu <= 3 * l_emu + 1e-3, (n, "l2", l_gpu, l_emu)
+        assert l_gpu <= 4 * l_emu + 1e-3, (n, "l2", l_gpu, l_emu)
         assert e_gpu <= 5 * e_emu + 1e-3, (n, "max", e_gpu, e_emu)
     # the step then applied Adam: every parameter moved, by at most ~lr (Adam's first-order bound)
     for n, p in tr.net.named_parameters():

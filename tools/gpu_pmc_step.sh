@@ -22,5 +22,9 @@ for SET in "${SETS[@]}"; do
 done
 python tools/pmc_step.py "$OUT" > "$OUT/pmc_step.txt"
 head -60 "$OUT/pmc_step.txt"
+# the probe kernel's HBM traffic per launch (bench.py's roofline "traffic"): the FETCH_SIZE / WRITE_SIZE passes
+ln -sfn pmc3 "$OUT/pmc_fetch" && ln -sfn pmc4 "$OUT/pmc_write"
+python tools/traffic.py "$OUT" > "$OUT/traffic.json"
+head -20 "$OUT/traffic.json"
 for d in "$OUT"/pmc[0-9]; do find "$d" -name '*counter_collection.csv' -size +2M -exec gzip {} \; ; done
 du -sh "$OUT"
