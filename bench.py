@@ -106,7 +106,8 @@ class Trainer:
     def forward_loss(self):
         with torch.autocast("cuda", dtype=self.dtype):
             out = self.model(self.images)
-        pred = torch.cat([o.float() for o in out], dim=1)
+        from sqr import tail
+        pred = tail.cat_heads(out)  # torch.cat of the heads (no copy: the fused tail packs them)
         loss = self.crit(self.images, pred)
         if self.crit_x is not None:
             loss = loss + self.crit_x(self.params, pred)

@@ -439,6 +439,9 @@ typedef struct sqr_tail_desc {
 size_t sqr_tail_save_floats(const sqr_tail_desc* t);
 int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a, float* out_e, float* out_t, float* out_q,
                  float* save, void* stream);
+/* the same with the four heads written side by side into pred [B][12] = (a, e, t, q): the
+ * reference's torch.cat of the heads (torch/train.py:88-89) without a copy */
+int sqr_tail_fwd_packed(const sqr_tail_desc* t, const void* x, float* pred, float* save, void* stream);
 typedef struct sqr_tail_grads {
   const float* g_out[4];  /* upstream grads of a, e, t, q: rows of ld[h] floats; NULL = zero */
   int ld[4];

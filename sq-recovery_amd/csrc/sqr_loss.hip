@@ -227,7 +227,7 @@ __device__ __forceinline__ void block_reduce_store(float* vals, float* red, floa
 // surface, where J is small too): relative error ~ eps * Ttot / suffix.  (Splitting a ray over 4
 // lanes, segment transmittances combined by lane scans, measured slower: 32 / 121 us.)
 // dyn LDS: axis[R] + reduction scratch.
-template <int NT, bool NEED_GRAD>
+template <int NT, bool NEED_GRAD, int UNR = 1>
 __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     const float* __restrict__ params, const float* __restrict__ target, int H, int W, int R,
     float tau, float sharp, float* __restrict__ partials) {
@@ -257,6 +257,7 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
 #pragma unroll
     for (int i = 0; i < (NEED_GRAD ? 17 : 1); ++i) JA[i] = JB[i] = 0.f;
     const float ntau = -tau * kLog2e;
+#pragma unroll UNR
     for (int k = 0; k < R; ++k) {
       const float gz = axis[R - 1 - k];
       Vox f;
@@ -592,11 +593,13 @@ extern "C" int sqr_implicit_loss_fwd_bwd_mean(const float* params, const float* 
   // (the gradient moments are computed whether or not they are wanted: the kernel without them
   // compiles the shared forward chain differently and its loss would differ in the last bits;
   // ImplicitLoss's value must not depend on torch.no_grad)
+  // (the depth loop unrolled by 2: two voxels' independent work interleaved; B = 64 call at R = 32
+  // 28.2 -> 25.7 us, config 5's R = 64 / B = 16 call 39.9 -> 37.3 us; unrolled by 4: the same)
   if (NT == 256)
-    hipLaunchKernelGGL((implicit_loss_kernel<256, true>), grid, dim3(256), lds, st, params, target, H, W, R, tau,
+    hipLaunchKernelGGL((implicit_loss_kernel<256, true, 2>), grid, dim3(256), lds, st, params, target, H, W, R, tau,
                        sharpness, partials);
   else
-    hipLaunchKernelGGL((implicit_loss_kernel<128, true>), grid, dim3(128), lds, st, params, target, H, W, R, tau,
+    hipLaunchKernelGGL((implicit_loss_kernel<128, true, 2>), grid, dim3(128), lds, st, params, target, H, W, R, tau,
                        sharpness, partials);
   SQR_HIP_LAUNCH_CHECK("implicit_loss_kernel");
   const double rr = (double)R * (double)R;

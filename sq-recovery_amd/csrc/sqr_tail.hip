@@ -33,6 +33,7 @@ constexpr int NOUT = 12;     // a(3) e(2) t(3) q(4)
 
 struct Dev {
   int B, P, C0, F1, F2, ldsave;
+  int ldout;  // 0: each head's output [B][n]; 12: one [B][12] prediction row per sample (a, e, t, q)
   const void* x;
   const float *w0, *b0, *w1, *b1;
   const float* wh[4];
@@ -196,12 +197,13 @@ __device__ __forceinline__ void heads_sample(const Dev& d, int n, const float* h
   __syncthreads();
   if (tid < NOUT) {
     const float zi = z[tid];
-    if (tid < 3) out_a[n * 3 + tid] = sigmoidf(zi);
-    else if (tid < 5) out_e[n * 2 + tid - 3] = sigmoidf(zi);
-    else if (tid < 8) out_t[n * 3 + tid - 5] = sigmoidf(zi);
+    const int ld = d.ldout;
+    if (tid < 3) out_a[n * (ld ? ld : 3) + tid] = sigmoidf(zi);
+    else if (tid < 5) out_e[n * (ld ? ld : 2) + tid - 3] = sigmoidf(zi);
+    else if (tid < 8) out_t[n * (ld ? ld : 3) + tid - 5] = sigmoidf(zi);
     else {
       const float nrm = sqrtf(z[8] * z[8] + z[9] * z[9] + z[10] * z[10] + z[11] * z[11]);
-      out_q[n * 4 + tid - 8] = zi / nrm;
+      out_q[n * (ld ? ld : 4) + tid - 8] = zi / nrm;
     }
   }
 }
@@ -479,6 +481,7 @@ Dev make_dev(const sqr_tail_desc* t, const void* x) {
   d.F1 = t->F1;
   d.F2 = t->F2;
   d.ldsave = t->C0 + t->F1 + t->F2 + NOUT;
+  d.ldout = 0;
   d.x = x;
   d.w0 = t->w0;
   d.b0 = t->b0;
@@ -502,12 +505,13 @@ extern "C" size_t sqr_tail_workspace_bytes(const sqr_tail_desc* t) {
   return (size_t)t->B * (t->F1 + t->F2 + NOUT) * sizeof(float);
 }
 
-extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a, float* out_e, float* out_t,
-                            float* out_q, float* save, void* stream) {
+static int tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a, float* out_e, float* out_t, float* out_q,
+                    int ldout, float* save, void* stream) {
   int rc = check_tail(t);
   if (rc) return rc;
   SQR_CHECK_ARG(x && out_a && out_e && out_t && out_q && save, "tail_fwd: null pointer");
-  const Dev d = make_dev(t, x);
+  Dev d = make_dev(t, x);
+  d.ldout = ldout;
   hipStream_t st = as_stream(stream);
   if (t->F1 % 16 == 0 && t->F2 % 16 == 0) {  // three launches, 4 workgroups per sample in fc0 / fc1
     if (t->dtype == SQR_DTYPE_BF16)
@@ -529,6 +533,16 @@ extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a,
     hipLaunchKernelGGL(tail_fwd_kernel<float>, dim3(t->B), dim3(256), 0, st, d, save, out_a, out_e, out_t, out_q);
   SQR_HIP_LAUNCH_CHECK("tail_fwd_kernel");
   return 0;
+}
+
+extern "C" int sqr_tail_fwd(const sqr_tail_desc* t, const void* x, float* out_a, float* out_e, float* out_t,
+                            float* out_q, float* save, void* stream) {
+  return tail_fwd(t, x, out_a, out_e, out_t, out_q, 0, save, stream);
+}
+
+extern "C" int sqr_tail_fwd_packed(const sqr_tail_desc* t, const void* x, float* pred, float* save, void* stream) {
+  SQR_CHECK_ARG(pred, "tail_fwd_packed: null pred");
+  return tail_fwd(t, x, pred, pred + 3, pred + 5, pred + 8, NOUT, save, stream);
 }
 
 extern "C" int sqr_tail_bwd(const sqr_tail_desc* t, const float* save, const sqr_tail_grads* g, void* workspace,

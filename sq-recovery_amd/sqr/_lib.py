@@ -168,6 +168,7 @@ SIGNATURES = {
     "sqr_tail_save_floats": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_fwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p]),
+    "sqr_tail_fwd_packed": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, c_void_p, c_void_p, c_void_p]),
     "sqr_tail_workspace_bytes": (c_size_t, [ctypes.POINTER(SqrTailDesc)]),
     "sqr_tail_bwd": (c_int, [ctypes.POINTER(SqrTailDesc), c_void_p, ctypes.POINTER(SqrTailGrads), c_void_p,
                              c_size_t, c_void_p]),

@@ -42,9 +42,12 @@ class TailFn(torch.autograd.Function):
         d = _desc(x, w0, b0, w1, b1, heads)
         L = lib()
         save = torch.empty(L.sqr_tail_save_floats(ctypes.byref(d)), dtype=torch.float32, device=x.device)
-        outs = [torch.empty(x.shape[0], n, dtype=torch.float32, device=x.device) for n in _HEAD_N]
-        check(L.sqr_tail_fwd(ctypes.byref(d), ptr(x), *[ptr(o) for o in outs], ptr(save), stream_ptr(x.device)),
-              "sqr_tail_fwd")
+        # the heads side by side in one [B, 12] row per sample (the reference's torch.cat order), each
+        # returned as a view: cat_heads then hands the whole buffer on without a copy
+        pred = torch.empty(x.shape[0], sum(_HEAD_N), dtype=torch.float32, device=x.device)
+        check(L.sqr_tail_fwd_packed(ctypes.byref(d), ptr(x), ptr(pred), ptr(save), stream_ptr(x.device)),
+              "sqr_tail_fwd_packed")
+        outs = pred.split(_HEAD_N, dim=1)
         ctx.pids = tuple(id(p) for p in params)
         ctx.save_for_backward(x, save, *params)
         return tuple(outs)
@@ -85,6 +88,41 @@ class TailFn(torch.autograd.Function):
             if go is None:
                 grads[4 + 2 * i] = grads[5 + 2 * i] = None
         return (dx, *grads)
+
+
+class _CatHeads(torch.autograd.Function):
+    """torch.cat((a, e, t, q), 1) of TailFn's outputs, which already lie side by side in one
+    [B, 12] buffer: that buffer as a view (no copy); the gradient goes back as its column views."""
+
+    @staticmethod
+    def forward(ctx, a, e, t, q):
+        return a.as_strided((a.shape[0], sum(_HEAD_N)), (sum(_HEAD_N), 1))
+
+    @staticmethod
+    def backward(ctx, g):
+        return tuple(g.split(_HEAD_N, dim=1))
+
+
+def _packed(outs):
+    if len(outs) != 4 or any(not isinstance(o, torch.Tensor) for o in outs):
+        return False
+    a = outs[0]
+    if not a.is_cuda or a.dim() != 2 or a.stride() != (sum(_HEAD_N), 1):
+        return False
+    off = a.storage_offset()
+    for o, n, c in zip(outs, _HEAD_N, (0, 3, 5, 8)):
+        if (o.dtype != torch.float32 or o.shape != (a.shape[0], n) or o.stride() != a.stride()
+                or o.untyped_storage().data_ptr() != a.untyped_storage().data_ptr() or o.storage_offset() != off + c):
+            return False
+    return True
+
+
+def cat_heads(outs):
+    """torch.cat([a, e, t, q], dim=1) as the reference forms its prediction (torch/train.py:88-89),
+    fp32; without a copy when the heads came out of the fused tail."""
+    if _packed(outs):
+        return _CatHeads.apply(*outs)
+    return torch.cat([o.float() for o in outs], dim=1)
 
 
 def supported(fc, heads):

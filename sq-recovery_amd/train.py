@@ -46,6 +46,7 @@ from sqr import amp, dist  # noqa: E402
 from sqr.data import DevicePrefetcher  # noqa: E402
 from sqr.optim import Adam  # noqa: E402
 from sqr.step import CapturedStep  # noqa: E402
+from sqr.tail import cat_heads  # noqa: E402
 
 
 def parse_args(argv=None):
@@ -147,7 +148,7 @@ def main(argv=None):
     def forward(x):
         with torch.autocast("cuda", dtype=amp_dtype or torch.bfloat16, enabled=amp_dtype is not None and use_cuda):
             out = model(x)
-        return torch.cat([o.float() for o in out], dim=1)
+        return cat_heads(out)  # torch.cat of the heads (train.py:88-89; no copy after the fused tail)
 
     def train_body(x, labels):
         pred_labels = forward(x)

@@ -85,3 +85,30 @@ def test_tail_deterministic():
                                                  heads[3].out_layer[0].weight.grad.clone()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_cat_heads_is_the_tail_buffer():
+    """cat_heads(outs) == torch.cat(outs, 1) with no copy (the fused tail writes the heads side by
+    side), and the backward through it gives every gradient bitwise as through torch.cat; a tuple
+    that is not the tail's packed buffer falls back to torch.cat."""
+    from sqr import tail
+    fc, heads = _modules(256, 3)
+    fc, heads = fc.to(DEV), [h.to(DEV) for h in heads]
+    x = torch.randn(64, 512, 8, 8, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.randn(64, 12, device=DEV)
+    res = []
+    for packed in (True, False):
+        xg = x.clone().requires_grad_(True)
+        for m in [fc, *heads]:
+            m.zero_grad(set_to_none=True)
+        outs = tail.resnet_tail(xg, fc, heads)
+        pred = tail.cat_heads(outs) if packed else torch.cat(outs, 1)
+        if packed:
+            assert pred.data_ptr() == outs[0].data_ptr() and pred.shape == (64, 12)
+        (pred.square() * w).sum().backward()
+        res.append([pred.detach().clone(), xg.grad.clone()] + [p.grad.clone() for m in [fc, *heads]
+                                                                 for p in m.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    loose = [torch.randn(4, n, device=DEV) for n in (3, 2, 3, 4)]
+    assert torch.equal(tail.cat_heads(loose), torch.cat(loose, 1))
