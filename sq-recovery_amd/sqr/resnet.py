@@ -39,12 +39,12 @@ class BasicBlock(nn.Module):
         # the identity / downsample branch's gradient of x is added in conv1's backward-data
         # epilogue through a ResidualJoin instead of a separate add)
         join = ResidualJoin.make(x)
-        # bn1's backward reduction in conv2's backward-data epilogue pays off up to 64x64 maps (the
-        # persistent layer-1 kernel at 256x256 input and every deeper layer); the tiled kernel on the
-        # 128x128 layer-1 maps of 512x512 input runs 118 -> 212 us with it (same-box A/B of config 5:
-        # +0.9 % without the link), so larger maps keep bn1's own reduction pass
+        # bn1's backward reduction in conv2's backward-data epilogue (BnBackwardLink).  Round 2 kept it
+        # off the 128x128 layer-1 maps of 512x512 input, where the tiled kernel ran 118 -> 212 us with
+        # it.  The persistent layer-1 kernel now covers 128-wide maps, so the link is on everywhere up
+        # to 128x128 (config 5 same-box A/B 9.49k -> 9.59k img/s, profiles/r04i_ab_c5_bnb_link128.txt).
         hw = (x.shape[2] // self.stride) * (x.shape[3] // self.stride)
-        link = BnBackwardLink.make(x, self.bn1) if hw <= 64 * 64 else None
+        link = BnBackwardLink.make(x, self.bn1) if hw <= 128 * 128 else None
         # x's producer (the previous block's output BatchNorm) may have its backward reduction ride
         # on conv1's weight-gradient launch (BnOutLink)
         red_link = getattr(x, "_sqr_outlink", None) if join is not None else None
