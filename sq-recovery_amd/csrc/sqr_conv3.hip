@@ -620,9 +620,12 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // sums of the values shifted by K = the channel's first value in pixel lane r32 = 0 (broadcast at
   // tile 0, shared by the wave's 32 pixel lanes of that channel, so their sums add exactly in the
   // final xor tree; no cancellation while the values stay within a few std of K)
-  LaneStat ls[STATS ? 16 : 1];
+  // STATS: this thread's 8 channels (slot tid & 7: every staged piece it stores holds them) summed
+  // over the pixels of its pieces as values shifted by the first one it stores (k, sum d, sum d^2),
+  // accumulated while the piece goes out -- inside the next tile's MFMA loop, not after it
+  float sk[STATS ? 8 : 1], ss[STATS ? 8 : 1], sq[STATS ? 8 : 1];
 #pragma unroll
-  for (int e = 0; e < (STATS ? 16 : 1); ++e) ls[e] = LaneStat{0.f, 0.f, 0.f};
+  for (int e = 0; e < (STATS ? 8 : 1); ++e) sk[e] = ss[e] = sq[e] = 0.f;
 
   u32x4 av[NST];  // ACC: the addend pieces of the tile stored next; BNB: the BatchNorm input x there
   uint32_t bm[(BNB || ACC) ? NST : 1];  // BNB / masked ACC: the mask byte of each piece (8 channels)
@@ -650,6 +653,24 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     {
       const int c = q * NT + tid, row = c >> 3, slot = c & 7;
       u32x4 v = *(const u32x4*)(stg + row * ROWB + ((slot ^ ((row ^ (row >> 3)) & 7)) << 4));
+      if constexpr (STATS) {
+        if (use) {
+          const bool first = k == 0 && q == 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = lo2f<T>(v[e]), hi = hi2f<T>(v[e]);
+            if (first) {
+              sk[2 * e] = lo;
+              sk[2 * e + 1] = hi;
+            }
+            const float d0 = lo - sk[2 * e], d1 = hi - sk[2 * e + 1];
+            ss[2 * e] += d0;
+            sq[2 * e] = fmaf(d0, d0, sq[2 * e]);
+            ss[2 * e + 1] += d1;
+            sq[2 * e + 1] = fmaf(d1, d1, sq[2 * e + 1]);
+          }
+        }
+      }
       if constexpr (ACC) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -775,26 +796,6 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         pk[i][g][0] = pack2<T>(acc[i][4 * g], acc[i][4 * g + 1]);
         pk[i][g][1] = pack2<T>(acc[i][4 * g + 2], acc[i][4 * g + 3]);
       }
-    if constexpr (STATS) {
-      if (k == 0) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            ls[4 * g + 2 * q].k = __shfl(lo2f<T>(pk[0][g][q]), lane & 32, 64);
-            ls[4 * g + 2 * q + 1].k = __shfl(hi2f<T>(pk[0][g][q]), lane & 32, 64);
-          }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            lane_stat_add(ls[4 * g + 2 * q], lo2f<T>(pk[i][g][q]), false);
-            lane_stat_add(ls[4 * g + 2 * q + 1], hi2f<T>(pk[i][g][q]), false);
-          }
-    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // all waves are done with tile k's rows and the staging area
 #pragma unroll
@@ -842,36 +843,21 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       a.stats[((size_t)blockIdx.x * 2 + q) * BN + col] = col_sum(red + sl * 16 + 8 * q + e, NT / 8, 8 * 16);
     }
   }
-  if constexpr (STATS) {  // xor tree over the 32 pixel lanes -> red[2][WAVES_M][64 channels] -> Welford row
+  if constexpr (STATS) {  // per thread (mean, M2) of its 8 channels -> red[256][16] -> the 32 rows of a slot
     float* red = (float*)ring;
-    const float ng = (float)(32 * TM * ntile);  // values per wave and channel
-    const float inv = 1.f / ng;
+    const float n = (float)(NST * ntile);  // values per thread and channel
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float m[4], q[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float sa = ls[4 * g + e].s, sq = ls[4 * g + e].q;
-#pragma unroll
-        for (int off = 1; off < 32; off <<= 1) {
-          sa += __shfl_xor(sa, off, 64);
-          sq += __shfl_xor(sq, off, 64);
-        }
-        const float sn = sa * inv;
-        m[e] = ls[4 * g + e].k + sn;
-        q[e] = fmaxf(sq - sa * sn, 0.f);
-      }
-      if (r32 == 0) {
-        float* r1 = red + wm * BN + wn * WN + 8 * g + 4 * h;
-        *(f32x4*)r1 = f32x4{m[0], m[1], m[2], m[3]};
-        *(f32x4*)(r1 + WAVES_M * BN) = f32x4{q[0], q[1], q[2], q[3]};
-      }
+    for (int e = 0; e < 8; ++e) {
+      const float sn = ss[e] / n;
+      red[tid * 16 + e] = sk[e] + sn;
+      red[tid * 16 + 8 + e] = fmaxf(sq[e] - ss[e] * sn, 0.f);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (tid < BN) {
+    if (tid < BN) {  // channel tid = slot sl, element e: rows tid' = sl + 8 r (fixed order)
+      const int sl = tid >> 3, e = tid & 7;
       float mean, m2;
-      lane_rows_merge(red + tid, red + WAVES_M * BN + tid, WAVES_M, BN, ng, &mean, &m2);
+      lane_rows_merge(red + sl * 16 + e, red + sl * 16 + 8 + e, NT / 8, 8 * 16, n, &mean, &m2);
       a.stats[((size_t)blockIdx.x * 2) * BN + tid] = mean;
       a.stats[((size_t)blockIdx.x * 2 + 1) * BN + tid] = m2;
       if (tid == 0) a.stats[(size_t)gridDim.x * 2 * BN + blockIdx.x] = (float)(TH * TW * ntile);
