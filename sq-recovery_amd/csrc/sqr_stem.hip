@@ -34,6 +34,7 @@
 // registers (8 fragments) for the whole kernel.
 #include <limits.h>
 #include <stdint.h>
+#include <type_traits>
 #include "sqr_common.h"
 
 namespace sqr {
@@ -51,6 +52,15 @@ constexpr int KC = 64;           // conv1 output channels
 constexpr int WPITCH = 72;       // LDS window row pitch (elements): 144 B, a multiple of 4 B
 constexpr int GRID_PERSIST = 512;  // persistent grids (fixed: the partial-sum order is part of the result)
 constexpr int PART_BWD = 2 * KC * KC + 2 * KC;  // T1, S (patch Gram matrix), T3, sum g
+
+// compile-time loop: f(std::integral_constant<int, I>{}) for I = B .. E-1
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 template <typename T> struct TT;
 template <> struct TT<bf16> {
@@ -446,7 +456,6 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
   float sg[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) sg[e] = 0.f;
-  const int oct = tid & 15;  // A^T items: taps j = (tid >> 4) + 16 k, pixel octet o = tid & 15
 
   // register prefetch of the next tile's input window and pooled-gradient inputs
   Window<TI, T, 14, 70, 1> pw;
@@ -478,16 +487,35 @@ __global__ void __launch_bounds__(256, 2) stem_bwd_kernel(const TI* __restrict__
     }
     __syncthreads();
     if (t + (int)gridDim.x < ntiles) fetch(t + gridDim.x);
-    // (a) A^T from the window
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int j = (tid >> 4) + 16 * k, r = j >> 3, s = j & 7;
-      const int p0 = oct * 8, py = p0 >> 5, px0 = p0 & 31;
-      const uint16_t* src = win + (2 * py + r) * WPITCH + 2 * px0 + s;
-      u32x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (uint32_t)src[4 * e] | ((uint32_t)src[4 * e + 2] << 16);
-      *(u32x4*)(AT + img_off(j, p0)) = v;
+    // (a) A^T from the window: thread = (tap row r, pixel row py, 8-pixel octet o8, tap half sh) writes
+    // taps j = 8r + 4sh + s' (s' < 4) of pixels p0 .. p0+7: A[p0 + i][j] = window[2py + r][2(8 o8 + i)
+    // + 4sh + s'], i.e. every other element of 24 consecutive ones read as three 16-B pieces (the two
+    // sh threads read the same pieces: a broadcast) and picked apart by byte permutes
+    {
+      const int sh = tid & 1, o8 = (tid >> 1) & 3, r = ((tid >> 6) << 1) | ((tid >> 3) & 1), py = (tid >> 4) & 3;
+      const char* src = (const char*)(win + (2 * py + r) * WPITCH) + 32 * o8;
+      const u32x4 a0 = *(const u32x4*)src, a1 = *(const u32x4*)(src + 16), a2 = *(const u32x4*)(src + 32);
+      // word k of the 20 elements from 4sh on (compile-time k: no register indexing)
+      auto word = [&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const uint32_t lo = k < 4 ? a0[k & 3] : (k < 8 ? a1[k & 3] : a2[k & 3]);
+        constexpr int k2 = k + 2;
+        const uint32_t hi = k2 < 4 ? a0[k2 & 3] : (k2 < 8 ? a1[k2 & 3] : a2[k2 & 3]);
+        return sh ? hi : lo;
+      };
+      const int p0 = py * 32 + 8 * o8;
+      static_for<0, 4>([&](auto spc) {
+        constexpr int sp = decltype(spc)::value;
+        u32x4 v;
+        static_for<0, 4>([&](auto mc) {  // elements x = sp + 4m and x + 2 of the 20
+          constexpr int x = sp + 4 * decltype(mc)::value;
+          // (x odd: the high halves of words x/2 and x/2 + 1; even: the low halves)
+          constexpr uint32_t sel = (x & 1) ? 0x07060302u : 0x05040100u;
+          v[decltype(mc)::value] = __builtin_amdgcn_perm(word(std::integral_constant<int, (x >> 1) + 1>{}),
+                                                         word(std::integral_constant<int, (x >> 1)>{}), sel);
+        });
+        *(u32x4*)(AT + img_off(8 * r + 4 * sh + sp, p0)) = v;
+      });
     }
     // (b) g = pooled gradient routed to its argmax pixel: pixel (py, px) of quad (qy, qx) is tap
     // (py - 2a + 1, px - 2b + 1) of pooling window (K + a, J + b), a, b in {0, 1}

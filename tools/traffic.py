@@ -24,9 +24,10 @@ PROBE_KEY = ["fwd", 64, 64, 3, 1]
 # different bytes and are reported separately
 # (rocprofv3 leaves some instances mangled — STATS is the first bool: ...IDF16bLb1E... — and
 # demangles others badly: the forward bf16 instance shows as "conv3p_kernel<bool _Accum, bool, E,
-# false, false>", the type and STATS eaten; the two trailing flags ACC = BNB = false single it out
-# among this step's instances: forward, dgrad + addend, dgrad + BatchNorm operands)
-FWD_RE = re.compile(r"conv3p_kernel(IDF16b?Lb1E|<[^<>]*?,\s*true,|<bool _Accum, bool, E, false, false>)")
+# false, false, 64, 2>", the type and STATS eaten; the two flags ACC = BNB = false before the tile
+# geometry single it out among this step's instances: forward, dgrad + addend, dgrad + BatchNorm
+# operands)
+FWD_RE = re.compile(r"conv3p_kernel(IDF16b?Lb1E|<[^<>]*?,\s*true,|<bool _Accum, bool, E, false, false(, \d+, \d+)?>)")
 
 
 def per_dispatch(root, counter, kernel):
@@ -49,7 +50,7 @@ def main():
     write = per_dispatch(os.path.join(out, "pmc_write"), "WRITE_SIZE", kernel)
     pick = [n for n in fetch if FWD_RE.search(n)] if kernel == DEFAULT_KERNEL else list(fetch)
     if not pick:
-        pick = list(fetch)
+        sys.exit("traffic.py: no forward instance of %s among %s" % (kernel, sorted(fetch)))
     fv = [v for n in pick for v in fetch.get(n, [])]
     wv = [v for n in pick for v in write.get(n, [])]
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
