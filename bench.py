@@ -255,7 +255,7 @@ def time_loss_call(crit, images, B, dev, reps=20):
 
 # the probe kernel's forward instance in rocprofv3 kernel names (tools/traffic.py FWD_RE: the
 # statistics-producing conv3p_kernel<T, STATS=true, ACC=false, BNB=false>, mangled or demangled)
-_PROBE_RE = r"conv3p_kernel(IDF16b?Lb1E|<[^<>]*?,\s*true,|<bool _Accum, bool, E, false, false(, \d+, \d+)?>)"
+_PROBE_RE = r"conv3p_kernel(IDF16b?Lb1ELb0ELb0ELi\d+ELi\d+ELb0E|<[^<>]*?,\s*true,\s*false,\s*false,\s*\d+,\s*\d+(,\s*false)?>|<bool _Accum, bool, E, false, false(, \d+, \d+(, false)?)?>)"
 
 
 def kernel_src_sha():

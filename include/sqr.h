@@ -177,6 +177,15 @@ size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
 int sqr_conv_set_direct(int mode);
 int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
                          int* stats_rows, void* workspace, size_t workspace_bytes, void* stream);
+/* sqr_conv2d_fwd_stats of x_act = relu(x_pre * scale + shift), the preceding BatchNorm + ReLU applied
+ * while the conv stages its input (a BasicBlock's bn1 -> relu -> conv2, torchvision resnet18 in
+ * torch/models.py:181).  coef = [scale C][shift C] (sqr_bn_fwd_finalize).  x_act and x_mask (1 bit per
+ * element, as sqr_bn_fwd writes it) are written as side outputs, bitwise what sqr_bn_apply writes.
+ * Persistent layer-1 shapes only (16-bit, C = K = 64, 3x3 / s1 / p1, 64- or 128-wide maps):
+ * SQR_E_UNSUPPORTED otherwise, nothing launched. */
+int sqr_conv2d_fwd_stats_bnin(const void* x_pre, const float* coef, void* x_act, uint8_t* x_mask,
+                              const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats, int* stats_rows,
+                              void* stream);
 /* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1
  * implicit GEMM per output-parity class (no work on structurally zero taps), all classes in one
  * launch; bf16 3x3/s2 shapes of ResNetSQ's layers 2-4 take the direct window kernel instead. */
@@ -282,6 +291,14 @@ int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, const float* 
                      const float* gamma, const float* beta, float* running_mean, float* running_var, float momentum,
                      float eps, const void* residual, int relu, void* y, uint8_t* relu_mask, float* save_mean,
                      float* save_invstd, void* workspace, size_t workspace_bytes, void* stream);
+/* sqr_bn_fwd_stats in two halves: the finalize (batch statistics -> save_mean / save_invstd, running
+ * statistics, coef = [scale C][shift C]) and the apply pass y = relu?(x * scale + shift [+ residual]);
+ * the apply half is skipped when the consuming conv applies on load (sqr_conv2d_fwd_stats_bnin). */
+int sqr_bn_fwd_finalize(const float* stats, int stats_rows, long long M, int C, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, float momentum, float eps, float* save_mean,
+                        float* save_invstd, float* coef, void* stream);
+int sqr_bn_apply(const void* x, long long M, int C, int dtype, const float* coef, const void* residual, int relu,
+                 void* y, uint8_t* relu_mask, void* stream);
 /* backward of sqr_bn_fwd (training statistics): g = dy * [y > 0] with the forward's relu_mask (NULL
  * when the forward had no ReLU); dx, dgamma = sum g*xhat, dbeta = sum g; dres (nullable) = g. */
 int sqr_bn_bwd(const void* dy, const uint8_t* relu_mask, const void* x, long long M, int C, int dtype, const float* gamma,

@@ -924,6 +924,37 @@ extern "C" int sqr_bn_fwd_stats(const void* x, long long M, int C, int dtype, co
                             relu_mask, save_mean, save_invstd, workspace, st, stats, stats_rows);
 }
 
+extern "C" int sqr_bn_fwd_finalize(const float* stats, int stats_rows, long long M, int C, const float* gamma,
+                                   const float* beta, float* running_mean, float* running_var, float momentum,
+                                   float eps, float* save_mean, float* save_invstd, float* coef, void* stream) {
+  int rc = check_mc(M, C, SQR_DTYPE_F32);
+  if (rc) return rc;
+  SQR_CHECK_ARG(stats && stats_rows > 0 && save_mean && save_invstd && coef, "bn_fwd_finalize: null pointer");
+  return bn_finalize_partials(stats, stats_rows, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                              save_mean, save_invstd, coef, as_stream(stream));
+}
+
+extern "C" int sqr_bn_apply(const void* x, long long M, int C, int dtype, const float* coef, const void* residual,
+                            int relu, void* y, uint8_t* relu_mask, void* stream) {
+  int rc = check_mc(M, C, dtype);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x && coef && y, "bn_apply: null pointer");
+  const int nvec = (int)(M * (C / 8));
+  hipStream_t st = as_stream(stream);
+  uint8_t* mask = relu ? relu_mask : nullptr;
+  if (dtype == SQR_DTYPE_BF16)
+    hipLaunchKernelGGL((apply_kernel<bf16>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const bf16*)x, (const bf16*)residual,
+                       coef, C, nvec, relu, (bf16*)y, mask);
+  else if (dtype == SQR_DTYPE_F16)
+    hipLaunchKernelGGL((apply_kernel<f16>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const f16*)x, (const f16*)residual,
+                       coef, C, nvec, relu, (f16*)y, mask);
+  else
+    hipLaunchKernelGGL((apply_kernel<float>), dim3(ew_grid(nvec)), dim3(256), 0, st, (const float*)x,
+                       (const float*)residual, coef, C, nvec, relu, (float*)y, mask);
+  SQR_HIP_LAUNCH_CHECK("bn apply_kernel");
+  return 0;
+}
+
 extern "C" int sqr_stem_fwd_stats(const void* x, int N, int H, int W, int C, int dtype, const float* stats,
                                   int stats_rows, const float* gamma, const float* beta, float* running_mean,
                                   float* running_var, float momentum, float eps, void* y, uint8_t* argmax,

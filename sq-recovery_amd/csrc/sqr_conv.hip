@@ -1320,6 +1320,29 @@ extern "C" int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, 
   return conv_fwd_impl(x, w_krsc, y, d, stats, stats_rows, workspace, workspace_bytes, stream);
 }
 
+extern "C" int sqr_conv2d_fwd_stats_bnin(const void* x_pre, const float* coef, void* x_act, uint8_t* x_mask,
+                                         const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
+                                         int* stats_rows, void* stream) {
+  Shape sh;
+  int rc = check_desc(d, &sh);
+  if (rc) return rc;
+  SQR_CHECK_ARG(x_pre && coef && x_act && x_mask && w_krsc && y && stats && stats_rows,
+                "conv2d_fwd_stats_bnin: null pointer");
+  if (!direct3(d, sh)) {
+    set_error("conv2d_fwd_stats_bnin: only 16-bit 3x3 / stride 1 / pad 1 convs");
+    return SQR_E_UNSUPPORTED;
+  }
+  const BnInArgs b = {coef, x_act, x_mask};
+  rc = conv3_launch(d->dtype, x_pre, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, as_stream(stream),
+                    nullptr, nullptr, 1, nullptr, &b);
+  if (rc == kNotHandled) {
+    set_error("conv2d_fwd_stats_bnin: only the persistent layer-1 kernel's shapes (64 -> 64 channels, 64- or "
+              "128-wide maps)");
+    return SQR_E_UNSUPPORTED;
+  }
+  return rc;
+}
+
 // dgrad parity class (ph, pw) of a stride-st conv: taps r = r0 + st*t with (ph + pad - r) % st == 0
 struct DgradClass {
   int r0, Rc, s0, Sc, Hc, Wc, off_h, off_w;

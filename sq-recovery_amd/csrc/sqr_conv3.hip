@@ -513,6 +513,9 @@ struct D3PArgs {
   const uint8_t* bn_mask;  // ... its ReLU mask (1 bit / element) and ...
   const float* bn_mean;    // ... its batch mean: out = dgrad * mask, stats = its backward sums
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
+  const float* in_coef;  // BNIN launches: x is the PRE-activation of the preceding BatchNorm + ReLU,
+  void* in_act;          // [2][64] its (scale, shift): the conv reads relu(x * scale + shift) and writes
+  uint8_t* in_mask;      // that activation (in_act) and its ReLU mask (1 bit / element) as side outputs
   int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
   unsigned long long* tp;  // nullable: clock probe slots
@@ -528,7 +531,12 @@ struct D3PArgs {
 // stored value is g = dgrad * [relu mask] and a.stats receives, per workgroup, the BatchNorm
 // backward sums (sum g, sum g*(x - mean)) — what sqr_bn_bwd's separate reduction pass would read
 // back.  x and the mask of tile k are prefetched like ACC's addend.
-template <typename T, bool STATS, bool ACC = false, bool BNB = false, int TW = 64, int TH = 2>
+// BNIN (forward with STATS): BatchNorm apply + ReLU on load.  Every input row piece is transformed in
+// registers before it enters the LDS ring -- the new rows of tile k+1 during tile k's MFMA loop, the
+// first tile's rows in the prologue -- except the zero padding (rows / columns outside the image stay
+// zero: the conv pads the activation, not its input), and the rows this band owns (not its halo rows)
+// are written out as the activation and its mask, bitwise what sqr_bn's apply pass writes.
+template <typename T, bool STATS, bool ACC = false, bool BNB = false, int TW = 64, int TH = 2, bool BNIN = false>
 __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   constexpr int C = 64, BN = 64, NW = 4, NT = 256, ROWB = 128;
   // 2 x 2 waves, each WM pixels x 32 channels = TM 32x32 MFMA accumulators
@@ -548,7 +556,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   static_assert(STG <= WB, "the staged tile fits the weight image's region");
   static_assert(2 * WAVES_M * 32 * BN * 4 <= RING && NT * 16 * 4 <= RING, "statistics scratch fits the ring");
   static_assert(NST <= 8, "store schedule");
+  static_assert(!BNIN || (STATS && !ACC && !BNB), "apply-on-load: forward launches only");
   __shared__ __attribute__((aligned(1024))) char smem[WB + RING];  // 108 / 140 KiB
+  __shared__ __attribute__((aligned(16))) float bnc[BNIN ? 128 : 4];  // BNIN: scale[64], shift[64]
   char* const wl = smem + RING;
   char* const ring = smem;
   char* const stg = wl;
@@ -610,6 +620,37 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       if (i * NW + NW <= nrows * PPR || p < nrows * PPR) {
         uint32_t vo;
         *(u32x4*)(ring + row_piece(r0, p, &vo)) = v[i];
+      }
+    }
+  };
+
+  // BNIN: piece p of the nrows rows from r0 (the lane's 16 B of it, as row_piece maps them) ->
+  // relu(v * scale + shift) in place; the band's own rows also go out as the activation + mask
+  auto bn_in_piece = [&](int r0, int nrows, int p, u32x4& v) {
+    if constexpr (BNIN) {
+      const int j = p / PPR, part = p - j * PPR;
+      const int row = r0 + j;
+      const int L = ((row + 1) & (NSLOT - 1)) * SLOTR + part * 8 + prow, w = part * 8 + prow - 1;
+      if (p < nrows * PPR && (unsigned)row < (unsigned)H && (unsigned)w < (unsigned)TW) {
+        const int cg = pslot ^ ((L >> 1) & 7);  // the 8 channels this lane's piece holds
+        const f32x4 s0 = *(const f32x4*)(bnc + 8 * cg), s1 = *(const f32x4*)(bnc + 8 * cg + 4);
+        const f32x4 t0 = *(const f32x4*)(bnc + 64 + 8 * cg), t1 = *(const f32x4*)(bnc + 64 + 8 * cg + 4);
+        uint32_t mb = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sc0 = e < 2 ? s0[2 * e] : s1[2 * e - 4], sc1 = e < 2 ? s0[2 * e + 1] : s1[2 * e - 3];
+          const float sh0 = e < 2 ? t0[2 * e] : t1[2 * e - 4], sh1 = e < 2 ? t0[2 * e + 1] : t1[2 * e - 3];
+          const float o0 = fmaxf(fmaf(lo2f<T>(v[e]), sc0, sh0), 0.f);
+          const float o1 = fmaxf(fmaf(hi2f<T>(v[e]), sc1, sh1), 0.f);
+          v[e] = pack2<T>(o0, o1);
+          mb |= (lo2f<T>(v[e]) > 0.f ? 1u : 0u) << (2 * e);
+          mb |= (hi2f<T>(v[e]) > 0.f ? 1u : 0u) << (2 * e + 1);
+        }
+        if (row >= hb && row < hb + TH * ntile) {
+          const size_t pix = ((size_t)img * H + row) * TW + w;
+          *(u32x4*)((char*)a.in_act + pix * C * 2 + cg * 16) = v;
+          a.in_mask[pix * 8 + cg] = (uint8_t)mb;
+        }
       }
     }
   };
@@ -709,6 +750,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   // rvb[t & 1]: the new rows of tile t, loaded during tile t-2's MFMA loop, written to the ring at the
   // end of tile t-1 (about 1.5 tiles of load latency hidden)
   u32x4 rvb[2][RPW];
+  if constexpr (BNIN) {
+    if (tid < 128) bnc[tid] = a.in_coef[tid];
+  }
   {
     u32x4 t0[PRW], wv[WPW];
     load_rows(hb - 1, TH + 2, t0, true);  // tile 0: rows hb-1 .. hb+TH
@@ -718,6 +762,12 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       const int tap = r / BN, n = r - tap * BN;
       wv[i] = __builtin_amdgcn_raw_buffer_load_b128(
           wsrd, (uint32_t)(((n * 9 + tap) * C) * 2 + ((pslot ^ ((r >> 1) & 7)) << 4)), 0, 0);
+    }
+    if constexpr (BNIN) {
+      __syncthreads();  // the coefficients
+#pragma unroll
+      for (int i = 0; i < PRW; ++i)
+        if (i * NW + NW <= (TH + 2) * PPR || i * NW + wave < (TH + 2) * PPR) bn_in_piece(hb - 1, TH + 2, i * NW + wave, t0[i]);
     }
     write_rows(hb - 1, TH + 2, t0);
 #pragma unroll
@@ -774,6 +824,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
       if (s % SSP == 1 && s / SSP < NST) store_piece(k - 1, k >= 1, s / SSP);
       if (s % RSP == 3 % RSP && s / RSP < RPW)
         load_row_piece(hb + TH * (k + 2) + 1, s / RSP, rvb[P], k + 2 < ntile);
+      if constexpr (BNIN)  // tile k+1's new rows (loaded during tile k-1), before they enter the ring
+        if (s % RSP == 5 % RSP && s / RSP < RPW && k + 1 < ntile)
+          bn_in_piece(hb + TH * (k + 1) + 1, TH, (s / RSP) * NW + wave, rvb[1 - P][s / RSP]);
       if constexpr (ACC || BNB)
         if (s % SSP == 5 % SSP && s / SSP < NST) load_addend_piece(k, s / SSP);
       if (s + PD < NSTEP) load(s + PD, qf[(s + PD) % (PD + 1)]);
@@ -1623,8 +1676,11 @@ bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
 
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb, int stride,
-                 const uint8_t* addend_mask) {
+                 const uint8_t* addend_mask, const BnInArgs* bnin) {
   if (addend_mask && (!addend || stride != 1)) return kNotHandled;
+  if (bnin && (stride != 1 || flip || addend || bnb || !stats || Cin != 64 || Nout != 64 || (W != 64 && W != 128) ||
+               H % (W == 64 ? 2 : 1) || !g_persist))
+    return kNotHandled;  // apply-on-load: the persistent layer-1 forward only
   if (g_direct == 0) return kNotHandled;
   if (stride == 2) {  // forward only (H, W: the input size)
     if (flip || addend || bnb || H % 2 || W % 2 || Cin % 64 || Nout % 64) return kNotHandled;
@@ -1696,6 +1752,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     p.bn_mask = bnb ? bnb->mask : nullptr;
     p.bn_mean = bnb ? bnb->mean : nullptr;
     p.stats = stats;
+    p.in_coef = bnin ? bnin->coef : nullptr;
+    p.in_act = bnin ? bnin->act : nullptr;
+    p.in_mask = bnin ? bnin->mask : nullptr;
     p.H = H;
     p.bpi = bpi;
     p.tpb = tpi / bpi;
@@ -1707,7 +1766,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     if (stats_rows) *stats_rows = grid;  // one partial row per workgroup
     probe_begin(st);
 #define SQR_D3P_LAUNCH(TW_, TH_)                                                                      \
-  if (bnb)                                                                                           \
+  if (bnin)                                                                                          \
+    hipLaunchKernelGGL((conv3p_kernel<T, true, false, false, TW_, TH_, true>), dim3(grid), dim3(256), 0, st, p); \
+  else if (bnb)                                                                                      \
     hipLaunchKernelGGL((conv3p_kernel<T, false, false, true, TW_, TH_>), dim3(grid), dim3(256), 0, st, p); \
   else if (stats)                                                                                    \
     hipLaunchKernelGGL((conv3p_kernel<T, true, false, false, TW_, TH_>), dim3(grid), dim3(256), 0, st, p); \

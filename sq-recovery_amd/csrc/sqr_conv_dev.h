@@ -164,9 +164,18 @@ struct BnbArgs {
 // stride 2 (forward only, flip 0, no addend / bnb): H, W are the input size
 // addend_mask (nullable, with addend, stride 1): the addend is added only where its bit is set (a
 // ReLU-masked gradient read as (dy, mask) instead of a materialised copy)
+// the preceding BatchNorm + ReLU applied on load (forward of the persistent layer-1 kernel only, with
+// stats): x is that BatchNorm's input, coef its [2][64] (scale, shift); the activation and its ReLU
+// mask are written out as side outputs
+struct BnInArgs {
+  const float* coef;
+  void* act;
+  uint8_t* mask;
+};
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st, const void* addend = nullptr,
-                 const BnbArgs* bnb = nullptr, int stride = 1, const uint8_t* addend_mask = nullptr);
+                 const BnbArgs* bnb = nullptr, int stride = 1, const uint8_t* addend_mask = nullptr,
+                 const BnInArgs* bnin = nullptr);
 // direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
 // addend_s2 (with addend): the addend is compact [N][Ho][Wo][C] and lands on the (even, even) dX

@@ -95,6 +95,12 @@ SIGNATURES = {
     "sqr_conv2d_stats_floats": (c_size_t, [ctypes.POINTER(SqrConvDesc)]),
     "sqr_conv2d_fwd_stats": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                      ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),
+    "sqr_conv2d_fwd_stats_bnin": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          ctypes.POINTER(SqrConvDesc), c_void_p, ctypes.POINTER(c_int), c_void_p]),
+    "sqr_bn_fwd_finalize": (c_int, [c_void_p, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "sqr_bn_apply": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                             c_void_p]),
     "sqr_conv2d_bwd_data": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                     c_size_t, c_void_p]),
     "sqr_conv2d_bwd_data_acc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc),

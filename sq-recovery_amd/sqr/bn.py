@@ -37,7 +37,7 @@ def _ws_bytes(M, C):
 class BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, rmean, rvar, residual, relu, training, momentum, eps, stats=None,
-                res_join=None, link=None, out_link=None):
+                res_join=None, link=None, out_link=None, defer=False):
         x = x.contiguous(memory_format=_CL)
         N, C, H, W = x.shape
         M = N * H * W
@@ -49,16 +49,27 @@ class BNActFn(torch.autograd.Function):
         invstd = torch.empty(C, **f32)
         # ReLU mask (1 bit per element) for the backward instead of keeping/reading y
         mask = torch.empty(M * C // 8, dtype=torch.uint8, device=x.device) if (relu and training) else None
-        n = _ws_bytes(M, C)
-        ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         rm = ptr(rmean) if rmean is not None else ctypes.c_void_p(0)
         rv = ptr(rvar) if rvar is not None else ctypes.c_void_p(0)
-        if training and stats is not None:  # batch statistics from the producing conv's epilogue
+        if training and stats is not None and defer and relu and residual is None:
+            # finalize only: the consuming conv applies scale / shift / ReLU while staging its input
+            # and writes y and its mask itself (sqr.conv, sqr_conv2d_fwd_stats_bnin)
+            coef = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            check(lib().sqr_bn_fwd_finalize(ptr(stats), stats.shape[0], ctypes.c_longlong(M), C, ptr(weight),
+                                            ptr(bias), rm, rv, ctypes.c_float(momentum), ctypes.c_float(eps),
+                                            ptr(mean), ptr(invstd), ptr(coef), stream_ptr(x.device)),
+                  "sqr_bn_fwd_finalize")
+            _pending[y.data_ptr()] = (x, coef, mask)
+        elif training and stats is not None:  # batch statistics from the producing conv's epilogue
+            n = _ws_bytes(M, C)
+            ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
             check(lib().sqr_bn_fwd_stats(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(stats), stats.shape[0],
                                          ptr(weight), ptr(bias), rm, rv, ctypes.c_float(momentum),
                                          ctypes.c_float(eps), ptr(residual), int(relu), ptr(y), ptr(mask), ptr(mean),
                                          ptr(invstd), ptr(ws), n, stream_ptr(x.device)), "sqr_bn_fwd_stats")
         else:
+            n = _ws_bytes(M, C)
+            ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
             check(lib().sqr_bn_fwd(ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(bias), rm, rv,
                                    ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(residual),
                                    int(relu), ptr(y), ptr(mask), ptr(mean), ptr(invstd), ptr(ws), n,
@@ -97,7 +108,7 @@ class BNActFn(torch.autograd.Function):
             if ctx.res_join is not None:
                 dres = ctx.res_join.deposit(dres)
             return dx, (g * xhat).sum((0, 2, 3)), g.sum((0, 2, 3)), None, None, dres, None, None, None, None, None, None, \
-                None, None
+                None, None, None
         dx = torch.empty_like(x, memory_format=_CL)
         # an identity block's residual share g = dy * mask goes to conv1's backward-data as (dy, mask)
         # (sqr.conv.MaskedGrad) instead of being written here, when conv1's backward is still to run
@@ -121,7 +132,7 @@ class BNActFn(torch.autograd.Function):
                 dres = dy
             if ctx.res_join is not None:
                 dres = ctx.res_join.deposit(dres)
-            return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
+            return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None
         got = ctx.link.take(dy) if ctx.link is not None else None
         if got is not None:  # the consuming conv's backward-data already masked g and reduced it
             g, st, coef, dg, db = got
@@ -129,12 +140,12 @@ class BNActFn(torch.autograd.Function):
                 check(lib().sqr_bn_bwd_apply(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(coef), ptr(dx),
                                              stream_ptr(x.device)), "sqr_bn_bwd_apply")
                 gradbuf.written(ctx.pids)
-                return dx, dg, db, None, None, None, None, None, None, None, None, None, None, None
+                return dx, dg, db, None, None, None, None, None, None, None, None, None, None, None, None
             check(lib().sqr_bn_bwd_stats(ptr(g), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(st), st.shape[0],
                                          ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                          stream_ptr(x.device)), "sqr_bn_bwd_stats")
             gradbuf.written(ctx.pids)
-            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
+            return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
         check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
@@ -145,7 +156,7 @@ class BNActFn(torch.autograd.Function):
             dres = dy
         if ctx.res_join is not None:
             dres = ctx.res_join.deposit(dres)
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None, None
 
 
 def count_batches(bns):
@@ -180,12 +191,15 @@ def _check_stats(stats, x):
     return stats
 
 
-def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=None, out_link=None):
+def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=None, out_link=None, defer=False):
     """relu?(bn(x) [+ residual]) with nn.BatchNorm2d `bn`'s parameters and running statistics.
     x may be a (y, partials) pair from a stats-producing conv: training mode then takes the batch
     statistics from the partials instead of reducing over y.  res_join: the residual input's
     sqr.conv.ResidualJoin (its gradient goes there instead of to autograd); link: a
-    sqr.conv.BnBackwardLink to the conv that consumes the output (see there)."""
+    sqr.conv.BnBackwardLink to the conv that consumes the output (see there).  defer (training,
+    ReLU, no residual): the output is only allocated; the sqr.conv.Conv2d that consumes it applies
+    the BatchNorm while staging its input and writes it (or applies it first where it cannot) --
+    the output must go straight to that conv."""
     x, stats = _split(x)
     training = bn.training or not bn.track_running_stats
     if training and bn.track_running_stats and not counted:
@@ -193,8 +207,30 @@ def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=N
     mom = _momentum(bn) if (training and bn.track_running_stats) else 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    return BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
-                         _check_stats(stats, x), res_join if residual is not None else None, link, out_link)
+    y = BNActFn.apply(x, bn.weight, bn.bias, rm, rv, residual, bool(relu), bool(training), mom, float(bn.eps),
+                      _check_stats(stats, x), res_join if residual is not None else None, link, out_link, bool(defer))
+    pend = _pending.pop(y.data_ptr(), None)
+    if pend is not None:
+        y._sqr_bnin = pend  # (BatchNorm input, coef, ReLU mask): sqr.conv applies it on load
+    return y
+
+
+# BNActFn outputs whose apply pass was deferred to the consuming conv, by data pointer (handed to the
+# output tensor by bn_act: a custom Function's forward cannot tag the tensor autograd returns)
+_pending = {}
+
+
+def apply_deferred(y):
+    """Write a deferred BatchNorm + ReLU output (bn_act(defer=True)) in place: the consumer of y
+    could not apply it on load.  No-op for any other tensor."""
+    pend = getattr(y, "_sqr_bnin", None)
+    if pend is None:
+        return
+    del y._sqr_bnin
+    x, coef, mask = pend
+    N, C, H, W = x.shape
+    check(lib().sqr_bn_apply(ptr(x), ctypes.c_longlong(N * H * W), C, _dt(x), ptr(coef), None, 1, ptr(y), ptr(mask),
+                             stream_ptr(x.device)), "sqr_bn_apply")
 
 
 def _operand(x, stats, weight, bias, rmean, rvar, momentum, eps, mean, invstd):

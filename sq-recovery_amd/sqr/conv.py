@@ -203,6 +203,25 @@ def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
     return (y, ws) if return_ws else y
 
 
+def conv2d_fwd_bnin(x_pre, coef, x_act, mask, w_krsc, d):
+    """(y, partials) of conv(relu(x_pre * scale + shift)) with the preceding BatchNorm applied while
+    the conv stages its input; x_act and mask receive that activation and its ReLU mask
+    (sqr_conv2d_fwd_stats_bnin).  None where the kernel does not take the shape (nothing written)."""
+    import ctypes
+    ho, wo = _out_hw(d)
+    dt = _TORCH_DT[d.dtype]
+    y = torch.empty((d.N, d.K, ho, wo), dtype=dt, device=x_pre.device, memory_format=_CL)
+    L = lib()
+    st = torch.empty(L.sqr_conv2d_stats_floats(ctypes.byref(d)), dtype=torch.float32, device=x_pre.device)
+    rows = ctypes.c_int()
+    rc = L.sqr_conv2d_fwd_stats_bnin(ptr(x_pre), ptr(coef), ptr(x_act), ptr(mask), ptr(w_krsc), ptr(y), ctypes.byref(d),
+                                     ptr(st), ctypes.byref(rows), stream_ptr(x_pre.device))
+    if rc == -2:  # SQR_E_UNSUPPORTED
+        return None
+    check(rc, "sqr_conv2d_fwd_stats_bnin")
+    return y, st[:rows.value * 2 * d.K].view(rows.value, 2, d.K)
+
+
 def conv2d_bwd_data(gy, w_crsk, d):
     import ctypes
     dt = _TORCH_DT[d.dtype]
@@ -510,6 +529,15 @@ class Conv2dFn(torch.autograd.Function):
         ctx.set_materialize_grads(False)
         N, C, H, W = x.shape
         K, _, R, S = weight.shape
+        # x may be a BatchNorm + ReLU output whose apply pass was deferred to this conv (sqr.bn.bn_act)
+        pend = getattr(x, "_sqr_bnin", None)
+        if pend is not None and not (x.dtype == dt and x.is_contiguous(memory_format=_CL) and want_stats
+                                     and bias is None):
+            from .bn import apply_deferred
+            apply_deferred(x)
+            pend = None
+        elif pend is not None:
+            del x._sqr_bnin
         xin = x.to(dt).contiguous(memory_format=_CL)
         d = _desc(N, C, H, W, K, R, S, stride, pad, dt)
         need_dx = ctx.needs_input_grad[0]
@@ -518,7 +546,18 @@ class Conv2dFn(torch.autograd.Function):
         else:
             krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
         stats = None
-        if want_stats and bias is None:
+        fused = None
+        if pend is not None:  # apply-on-load: xin (= x) and the mask are written by the conv itself
+            x_pre, coef, mask = pend
+            with _Probe("fwd_bnin", d):
+                fused = conv2d_fwd_bnin(x_pre, coef, xin, mask, krsc, d)
+            if fused is None:  # not this kernel's shape: the apply pass first
+                x._sqr_bnin = pend
+                from .bn import apply_deferred
+                apply_deferred(x)
+        if fused is not None:
+            (y, stats), ws = fused, None
+        elif want_stats and bias is None:
             y, stats, ws = conv2d_fwd(xin, krsc, d, return_ws=True, stats=True)
         else:
             y, ws = conv2d_fwd(xin, krsc, d, return_ws=True)

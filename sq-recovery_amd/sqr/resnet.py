@@ -16,6 +16,9 @@ from .bn import bn_act, bn_add_act, count_batches, fused_stem, fused_stem_ok, st
 from .conv import BnBackwardLink, BnOutLink, Conv2d, ResidualJoin, compute_dtype, pack_all
 
 
+_BN_DEFER = os.environ.get("SQR_BN_DEFER", "1") != "0"  # A/B switch (1 = apply-on-load where possible)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -48,8 +51,10 @@ class BasicBlock(nn.Module):
         # x's producer (the previous block's output BatchNorm) may have its backward reduction ride
         # on conv1's weight-gradient launch (BnOutLink)
         red_link = getattr(x, "_sqr_outlink", None) if join is not None else None
+        # bn1 -> ReLU is applied by conv2 while it stages its input (apply-on-load, where its kernel
+        # takes the shape; sqr.bn.bn_act(defer=True)): no separate apply pass over conv1's output
         out = bn_act(self.conv1.forward_stats(x, self.bn1, join=join, role="acc", bnr=red_link), self.bn1, relu=True,
-                     counted=True, link=link)
+                     counted=True, link=link, defer=_BN_DEFER)
         out_link = BnOutLink(2 if self.downsample is not None else 1) if join is not None else None
         if self.downsample is not None:
             # bn2(conv2) + bn_ds(conv_ds) + ReLU as ONE op: the downsample branch is never normalised

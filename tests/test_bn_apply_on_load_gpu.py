@@ -1,0 +1,81 @@
+"""BatchNorm + ReLU applied on load by the persistent layer-1 conv (sqr_conv2d_fwd_stats_bnin:
+bn1 -> relu -> conv2 of a BasicBlock, torch/models.py:181) against the two-pass path it replaces
+(sqr_bn_apply, then sqr_conv2d_fwd_stats): the activation, its ReLU mask, the conv output and its
+BatchNorm partials bitwise equal -- the same arithmetic on the same values, the zero padding left
+alone -- at the config-2 (64 x 64 maps, B=64) and config-5 (128 x 128, B=16) shapes."""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("N,H", [(64, 64), (16, 128), (2, 64), (1, 128)])
+def test_conv_bnin_equals_apply_then_conv(N, H, dtype):
+    from sqr import conv as sc
+    from sqr._lib import check, lib, ptr, stream_ptr
+    L = lib()
+    g = torch.Generator(device=DEV).manual_seed(N * 7 + H)
+    C = 64
+    x_pre = (torch.randn(N, C, H, H, device=DEV, generator=g) * 2 + 0.3).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    coef = torch.cat([torch.randn(C, device=DEV, generator=g) * 0.8,      # scale (some negative)
+                      torch.randn(C, device=DEV, generator=g) * 0.5])    # shift
+    w = torch.randn(C, C, 3, 3, device=DEV, generator=g) / 24.0
+    d = sc._desc(N, C, H, H, C, 3, 3, 1, 1, dtype)
+    krsc, _ = sc.pack_weight(w, d, False)
+    st = stream_ptr(torch.device(DEV))
+    M = N * H * H
+    # two passes: the BatchNorm apply, then the conv on its output
+    a_ref = torch.empty_like(x_pre)
+    m_ref = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    check(L.sqr_bn_apply(ptr(x_pre), ctypes.c_longlong(M), C, sc._DT[dtype], ptr(coef), None, 1, ptr(a_ref), ptr(m_ref),
+                         st), "apply")
+    y_ref, s_ref = sc.conv2d_fwd(a_ref, krsc, d, stats=True)
+    # one pass: applied while staging
+    a = torch.full_like(x_pre, float("nan"))
+    m = torch.full((M * C // 8,), 0x5A, dtype=torch.uint8, device=DEV)
+    y, s = sc.conv2d_fwd_bnin(x_pre, coef, a, m, krsc, d)
+    torch.cuda.synchronize()
+    assert torch.equal(a, a_ref)
+    assert torch.equal(m, m_ref)
+    assert torch.equal(y, y_ref)
+    assert s.shape == s_ref.shape and torch.equal(s, s_ref)
+
+
+def test_conv_bnin_declines_other_shapes():
+    from sqr import conv as sc
+    x = torch.zeros(2, 128, 32, 32, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    d = sc._desc(2, 128, 32, 32, 128, 3, 3, 1, 1, torch.bfloat16)
+    krsc, _ = sc.pack_weight(torch.zeros(128, 128, 3, 3, device=DEV), d, False)
+    coef = torch.zeros(256, device=DEV)
+    a = torch.empty_like(x)
+    m = torch.empty(2 * 32 * 32 * 128 // 8, dtype=torch.uint8, device=DEV)
+    assert sc.conv2d_fwd_bnin(x, coef, a, m, krsc, d) is None
+
+
+@pytest.mark.parametrize("config", [2, 5])
+def test_block_step_with_apply_on_load_equals_without(config):
+    """The bench step (one eager forward + backward) with bn1 applied on load and with its separate
+    apply pass: the same loss and every gradient bitwise (run in two child processes: the switch is
+    read at import)."""
+    import os
+    import subprocess
+    import sys
+    import tempfile
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with tempfile.TemporaryDirectory() as tmp:
+        outs = []
+        for on in ("1", "0"):
+            out = os.path.join(tmp, "g%s.pt" % on)
+            env = dict(os.environ, SQR_BN_DEFER=on)
+            subprocess.run([sys.executable, os.path.join(root, "tools", "step_grads.py"), out, str(config)], env=env,
+                           check=True, timeout=300)
+            outs.append(torch.load(out, weights_only=True))
+        a, b = outs
+        assert a["loss"] == b["loss"]
+        for n in a["grads"]:
+            assert torch.equal(a["grads"][n], b["grads"][n]), n
