@@ -172,6 +172,10 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 // (a, .) holding TH+1-a rows.  Tap (r, c) of output pixel (y, x) reads plane (r & 1, c & 1) at
 // (y + (r >> 1), x + (c >> 1)): consecutive output pixels are consecutive plane rows and the tap
 // offset is one constant per tap, so the stride-1 fragment reads carry over unchanged.
+// SQR_D3_WINPF: read the next tap's first window fragments before each step's barrier
+#ifndef SQR_D3_WINPF
+#define SQR_D3_WINPF 1
+#endif
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2,
           bool ACC = false, bool BNB = false, int S = 1>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
@@ -328,6 +332,30 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   }
   __builtin_amdgcn_s_barrier();
 
+  // window fragment offsets of tap t (r, c3) for this lane's TM pixel rows
+  auto tap_qoff = [&](int t, int* qo) {
+    const int r = t / 3, c3 = t % 3;
+    int toff;
+    if constexpr (S == 1) {
+      toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
+    } else {
+      toff = ((r & 1) ? 2 * P0 + (c3 & 1) * P1 : (c3 & 1) * P0) + (r >> 1) * WWID + (c3 >> 1);
+    }
+    // K20: tap offset toff = 10 r' + c' (r', c' the possibly flipped tap) is 10 (r' & 1) + c' mod 20
+    const int kj = K20 ? 3 * ((flip ? 2 - c3 : c3) + 3 * ((flip ? 2 - r : r) & 1)) : 0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int row = qbase[i] + toff;
+      // keep the per-tap address math here: hoisted for all 9 unrolled taps it spills
+      asm volatile("" : "+v"(row));
+      const int key = K20 ? (qkey[i] >> kj) & 7 : d3key(row);
+      qo[i] = row * ROWB + ((fq ^ key) << 4);
+    }
+  };
+  constexpr bool kWinPrefetch = SQR_D3_WINPF;
+  int qoff_n[TM];
+  V8<T> qn[TM];
+
   for (int cc = 0; cc < nch; ++cc) {
     const bool next = cc + 1 < nch;
     const char* win = smem + (NWB == 2 ? (cc & 1) * WIN : 0);
@@ -352,24 +380,15 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
           dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff,
                              __builtin_amdgcn_readfirstlane((next ? cc + 1 : cc) * 128), wave);
       }
-      const int r = t / 3, c3 = t % 3;
-      int toff;
-      if constexpr (S == 1) {
-        toff = flip ? (2 - r) * WWID + (2 - c3) : r * WWID + c3;
-      } else {
-        toff = ((r & 1) ? 2 * P0 + (c3 & 1) * P1 : (c3 & 1) * P0) + (r >> 1) * WWID + (c3 >> 1);
-      }
       const char* bst = bring + (PD == 2 ? (t % 3) : (step % STAGES)) * TILE_B;
       int qoff[TM];
-      // K20: tap offset toff = 10 r' + c' (r', c' the possibly flipped tap) is 10 (r' & 1) + c' mod 20
-      const int kj = K20 ? 3 * ((flip ? 2 - c3 : c3) + 3 * ((flip ? 2 - r : r) & 1)) : 0;
+      if constexpr (kWinPrefetch) {
+        if (t == 0) tap_qoff(0, qoff);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        int row = qbase[i] + toff;
-        // keep the per-tap address math here: hoisted for all 9 unrolled taps it spills
-        asm volatile("" : "+v"(row));
-        const int key = K20 ? (qkey[i] >> kj) & 7 : d3key(row);
-        qoff[i] = row * ROWB + ((fq ^ key) << 4);
+        for (int i = 0; i < TM; ++i)
+          if (t > 0) qoff[i] = qoff_n[i];
+      } else {
+        tap_qoff(t, qoff);
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
@@ -377,17 +396,37 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
         for (int j = 0; j < TN; ++j) pf[j] = *(const V8<T>*)(bst + (poff[j] ^ (sub << 6)));
 #pragma unroll
-        for (int i = 0; i < TM; ++i) qf[i] = *(const V8<T>*)(win + (qoff[i] ^ (sub << 6)));
+        for (int i = 0; i < TM; ++i)
+          qf[i] = kWinPrefetch && sub == 0 && t > 0 ? qn[i] : *(const V8<T>*)(win + (qoff[i] ^ (sub << 6)));
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
       }
+      // the next tap's first window fragments, read before this step's barrier: the window of a
+      // chunk is stable through its 9 taps (only the weight stage needs the barrier), so after it
+      // only the weight fragments' LDS latency stands between the barrier and the first MFMA
+      if constexpr (kWinPrefetch) {
+        if (t < 8) {
+          tap_qoff(t + 1, qoff_n);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) qn[i] = *(const V8<T>*)(win + qoff_n[i]);
+        }
+      }
+      // the window prefetch (TM reads, the youngest LDS operations) stays in flight over the barrier
+      const bool pre = kWinPrefetch && t < 8;
       // Every step-end wait also retires this wave's own LDS reads (lgkmcnt(0)): the raw s_barrier
       // does not wait for them on gfx950, and after it other waves DMA into the stage just read —
       // an LDS-DMA write is not ordered behind another wave's queued ds_read, so a read still in
       // the LDS queue could see the next tile (seen as a rare wrong 16-channel fragment at B = 16
       // with two workgroups per CU; the epilogue's reuse of the LDS for statistics relies on it too)
+#define SQR_D3_STEP_WAIT(V)                                                                  \
+  do {                                                                                       \
+    if (pre)                                                                                 \
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(%1)" ::"n"(V), "n"(TM) : "memory");          \
+    else                                                                                     \
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(V) : "memory");                     \
+  } while (0)
       if constexpr (PD == 2) {
         const bool more = t < 7 || next;
         // retire the weight tile of the next step (and at tap 8 the next window, which is older);
@@ -395,19 +434,20 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
         if (!more) {
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         } else if (NWB == 2 && t <= 1 && next) {
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB + WP) : "memory");
+          SQR_D3_STEP_WAIT(PB + WP);
         } else {
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB) : "memory");
+          SQR_D3_STEP_WAIT(PB);
         }
       } else {
         // retire weight tile step+1 (issued at step+1-PD): younger are tiles step+2 .. step+PD and,
         // for t <= PD-1, this chunk's window load (issued at t = 0 after that step's tile load)
         if (t <= PD - 1) {
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1) + WP) : "memory");
+          SQR_D3_STEP_WAIT(PB * (PD - 1) + WP);
         } else {
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
+          SQR_D3_STEP_WAIT(PB * (PD - 1));
         }
       }
+#undef SQR_D3_STEP_WAIT
       __builtin_amdgcn_s_barrier();
     }
   }
@@ -474,10 +514,21 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
                                                a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0);
   }
   uint16_t* out = (uint16_t*)a.out;
+  // 16-B stores: a lane holds 4 channels (8 B) of each 16-channel tile j; v_permlane16_swap of the
+  // tile pair (j, j+1) trades the odd 16-lane rows (fq = 1, 3) of tile j against the even rows of
+  // tile j+1, after which lane (fr, fq) holds the 8 contiguous channels 16 (j + (fq & 1)) + 8 (fq >> 1)
+  // .. +7 of its pixel: half the store instructions for the same bytes (the tail of this epilogue is
+  // store-issue bound with every CU's workgroup storing at once)
+  static_assert(TN % 2 == 0, "tile pairs");
+  const int sw = 12 * (fq & 1);  // 16 (fq & 1) + 8 (fq >> 1) - 4 fq
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) *(u32x2*)(out + opix[i] + 16 * j) = u32x2{pk[j][i][0], pk[j][i][1]};
+    for (int j = 0; j < TN; j += 2) {
+      const auto r0 = __builtin_amdgcn_permlane16_swap(pk[j][i][0], pk[j + 1][i][0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(pk[j][i][1], pk[j + 1][i][1], false, false);
+      *(u32x4*)(out + opix[i] + 16 * j + sw) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+    }
   if (!BNB && a.stats)
     tile_stats<T, BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
                                                  a.stats + ((size_t)tile_m * 2) * a.Nout + n0,
