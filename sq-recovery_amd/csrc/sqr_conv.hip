@@ -277,14 +277,39 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
       orow[i] = ((size_t)n * a.oH + oi * a.os + a.oph) * a.oW + oj * a.os + a.opw;
     }
   }
+  bool wide = false;
+  if constexpr (C::ES == 2 && TN % 2 == 0) wide = a.Nout % 8 == 0;
+  if constexpr (C::ES == 2 && TN % 2 == 0) {
+    if (wide) {
+      // 16-bit output in 16-B stores: v_permlane16_swap of tile pair (j, j+1) leaves lane (fr, fq)
+      // the 8 contiguous channels 16 (j + (fq & 1)) + 8 (fq >> 1) .. +7 of its pixel (as in the
+      // direct 3x3 kernels' epilogue: half the store instructions, same bytes)
+      const int sw = 12 * (fq & 1);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + 16 * j + 4 * fq;
-    if (n >= a.Nout) continue;
+      for (int j = 0; j + 1 < TN; j += 2) {
+        const int n = n0 + wn * WN + 16 * j + 4 * fq + sw;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WM + 16 * i + fr;
-      if (m < g.M) store4(out + orow[i] * a.Nout + n, acc[j][i]);
+        for (int i = 0; i < TM; ++i) {
+          const auto r0 = __builtin_amdgcn_permlane16_swap(pack2<T>(acc[j][i][0], acc[j][i][1]),
+                                                           pack2<T>(acc[j + 1][i][0], acc[j + 1][i][1]), false, false);
+          const auto r1 = __builtin_amdgcn_permlane16_swap(pack2<T>(acc[j][i][2], acc[j][i][3]),
+                                                           pack2<T>(acc[j + 1][i][2], acc[j + 1][i][3]), false, false);
+          const int m = m0 + wm * WM + 16 * i + fr;
+          if (m < g.M && n < a.Nout) *(u32x4*)(out + orow[i] * a.Nout + n) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+        }
+      }
+    }
+  }
+  if (!wide) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + 16 * j + 4 * fq;
+      if (n >= a.Nout) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WM + 16 * i + fr;
+        if (m < g.M) store4(out + orow[i] * a.Nout + n, acc[j][i]);
+      }
     }
   }
   if (a.stats) {
