@@ -362,24 +362,30 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int step = cc * 9 + t;
-      if constexpr (PD == 2) {
-        // (the original 3-stage schedule: no loads past the end)
-        if (t < 7) {
-          dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff,
-                             __builtin_amdgcn_readfirstlane(((t + 2) * a.Cin + cc * 64) * 2), wave);
-        } else if (next) {
-          dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff,
-                             __builtin_amdgcn_readfirstlane(((t - 7) * a.Cin + (cc + 1) * 64) * 2), wave);
+      // this step's LDS-DMA issue (the weight tile PD steps ahead, at tap 0 the next chunk's window),
+      // placed after the step's MFMAs: issued among them it costs the waves more issue cycles
+      // (same-box kernel timings: 0.3-0.8 us less per launch on layers 2-3, 1.4 % over the nine
+      // tiled shapes, profiles/r04dp_tiled_conv_dma_position.jsonl)
+      auto issue_step = [&]() {
+        if constexpr (PD == 2) {
+          // (the original 3-stage schedule: no loads past the end)
+          if (t < 7) {
+            dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff,
+                               __builtin_amdgcn_readfirstlane(((t + 2) * a.Cin + cc * 64) * 2), wave);
+          } else if (next) {
+            dma_pieces<PB, NW>(wsrd, bring + ((t + 2) % 3) * TILE_B, bvoff,
+                               __builtin_amdgcn_readfirstlane(((t - 7) * a.Cin + (cc + 1) * 64) * 2), wave);
+          }
+          if (NWB == 2 && t == 0 && next)
+            dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff, __builtin_amdgcn_readfirstlane((cc + 1) * 128),
+                               wave);
+        } else {
+          issue_w(step + PD);
+          if (t == 0)  // next chunk's window (the last chunk reloads its own into the idle buffer)
+            dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff,
+                               __builtin_amdgcn_readfirstlane((next ? cc + 1 : cc) * 128), wave);
         }
-        if (NWB == 2 && t == 0 && next)
-          dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff, __builtin_amdgcn_readfirstlane((cc + 1) * 128),
-                             wave);
-      } else {
-        issue_w(step + PD);
-        if (t == 0)  // next chunk's window (the last chunk reloads its own into the idle buffer)
-          dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff,
-                             __builtin_amdgcn_readfirstlane((next ? cc + 1 : cc) * 128), wave);
-      }
+      };
       const char* bst = bring + (PD == 2 ? (t % 3) : (step % STAGES)) * TILE_B;
       int qoff[TM];
       if constexpr (kWinPrefetch) {
@@ -403,6 +409,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
           for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
       }
+      issue_step();
       // the next tap's first window fragments, read before this step's barrier: the window of a
       // chunk is stable through its 9 taps (only the weight stage needs the barrier), so after it
       // only the weight fragments' LDS latency stands between the barrier and the first MFMA
