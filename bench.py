@@ -22,6 +22,7 @@ same inside-outside model (values in [0,1], background 0).
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import contextlib
 import json
 import os
 import platform
@@ -63,7 +64,7 @@ class Trainer:
     step's gradients against a float64 reference)."""
 
     def __init__(self, dev, config=2, batch=64, render=0, dtype=None, graph=True, rank=0, world=1, seed=1234,
-                 dp_rehearsal=False):
+                 dp_rehearsal=False, dp_overlap=True):
         import classes
         import models
         from sqr import amp, dist
@@ -71,11 +72,17 @@ class Trainer:
         from sqr import optim as sqr_optim
         self.dev, self.config, self.B, self.world = dev, config, batch, world
         self.H, self.R, cdt = config_shape(config, render)
-        self.dtype = dtype or cdt
-        rng = np.random.default_rng(seed + rank)
-        self.params = torch.tensor(classes.sample_sq_params(rng, batch), device=dev)
-        # [B,1,H,H] in [0,1]
-        self.images = losses.implicit_render(self.params, self.H, 1.5, 260).unsqueeze(1).contiguous()
+        self.cuda = torch.device(dev).type == "cuda"
+        # the host path (--device cpu: the launcher's CPU test) computes in fp32 like the reference
+        self.dtype = (dtype or cdt) if self.cuda else torch.float32
+        if self.cuda:
+            rng = np.random.default_rng(seed + rank)
+            self.params = torch.tensor(classes.sample_sq_params(rng, batch), device=dev)
+            # [B,1,H,H] in [0,1]
+            self.images = losses.implicit_render(self.params, self.H, 1.5, 260).unsqueeze(1).contiguous()
+        else:
+            ds = classes.SyntheticDataset(batch, dev, 1.0, self.H, seed + rank)
+            self.params, self.images = ds.labels, ds.images
 
         torch.manual_seed(0)  # identical init on every rank (the data-parallel wrappers also broadcast)
         self.net = models.ResNetSQ(outputs=4, pretrained=False).to(dev)
@@ -88,7 +95,7 @@ class Trainer:
         self.crit_x = classes.ExplicitLoss(32, dev) if config == 4 else None
         # fp16: dynamic loss scaling (GradScaler semantics, device-resident, graph-capturable)
         self.scaler = amp.GradScaler() if self.dtype == torch.float16 else None
-        self.use_graph = graph
+        self.use_graph = graph and self.cuda
         self.gdp = None
         self.model = self.net
         # dp_rehearsal: the N>1 path (flat buffer, bucket hooks, captured RCCL all-reduce) at N=1 on a
@@ -97,14 +104,15 @@ class Trainer:
             dist.open_comm(dev)
         if world > 1 or dp_rehearsal:
             # the same data path captured (default) or eager (--graph 0); no other fallback
-            self.gdp = dist.GraphDataParallel(self.net, self.opt, dev)
+            self.gdp = dist.GraphDataParallel(self.net, self.opt, dev, overlap=dp_overlap)
         self.grad_seed = torch.ones((), dtype=torch.float64, device=dev)
         self.graph = None
         self.static_loss = None
         self._step = self.eager_step
 
     def forward_loss(self):
-        with torch.autocast("cuda", dtype=self.dtype):
+        ctx = torch.autocast("cuda", dtype=self.dtype) if self.cuda else contextlib.nullcontext()
+        with ctx:
             out = self.model(self.images)
         from sqr import tail
         pred = tail.cat_heads(out)  # torch.cat of the heads (no copy: the fused tail packs them)
@@ -400,9 +408,41 @@ def cpu_baseline(images_cpu, params_cpu, state_dict, R, steps, cfg1_steps):
     return out
 
 
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` without a torchrun environment: this process becomes the launcher.  It
+    starts N fresh rank processes (torch.distributed.run, one per GPU, rendezvous on 127.0.0.1),
+    relays the one JSON line rank 0 prints and returns the launcher's exit code (non-zero when any
+    rank failed).  Nothing here touches HIP: the parent never initialises a GPU, so the ranks own
+    their devices from the start (and no GPU-initialised process ever replaces itself)."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (the host driver has no legacy IPC)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, cpu_quota() // n)))
+    print("bench: launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)  # stderr streams through
+    lines = [ln for ln in proc.stdout.decode(errors="replace").splitlines() if ln.lstrip().startswith("{")]
+    rc = proc.returncode
+    if len(lines) == 1:
+        print(lines[0], flush=True)
+    else:  # no line (a rank died before printing) or several: one line naming the failure
+        print(json.dumps({"metric": "training images/sec", "value": None, "unit": "images/s", "n_gpus": n,
+                          "dp_error": "launcher: %d JSON lines from the ranks, exit code %d" % (len(lines), rc),
+                          "rank_lines": lines[:4]}), flush=True)
+        rc = rc or 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); > 1 without a torchrun environment launches them itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
@@ -416,22 +456,62 @@ def main():
                          "baseline), so the last --steps step graphs of the trace are the timed ones")
     ap.add_argument("--dp-rehearsal", action="store_true",
                     help="N=1 only: run the data-parallel machinery (captured RCCL all-reduce) on a world-1 group")
+    ap.add_argument("--dp-overlap", type=int, default=1, choices=(0, 1),
+                    help="1: bucketed all-reduces on a side stream during the backward; 0: one all-reduce of the "
+                         "whole gradient buffer after the backward, on the compute stream")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole train step in a HIP graph (1/0; default: on)")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
+                    help="cpu: the host path over gloo, eager (launcher / data-parallel plumbing tests only)")
     args = ap.parse_args()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if world_env is not None and int(world_env) != args.gpus:
+        # a torchrun world that disagrees with --gpus would report a curve point for the wrong N
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"metric": "training images/sec", "value": None, "unit": "images/s",
+                              "n_gpus": int(world_env),
+                              "dp_error": "WORLD_SIZE=%s but --gpus %d" % (world_env, args.gpus)}), flush=True)
+        sys.exit(2)
     # stdout carries exactly ONE line (the JSON result): native libraries that print to fd 1 (RCCL's
     # version banner at communicator init) are redirected to stderr; the JSON goes to a saved fd
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    try:
+        run(args, json_fd)
+    except Exception as e:
+        from sqr import dist
+        if isinstance(e, dist.CommFailure):
+            # the communicator is aborted; no orderly teardown can follow (peers may be gone)
+            import traceback
+            traceback.print_exc()
+            if dist.env()[0] == 0:
+                os.write(json_fd, (json.dumps({"metric": "training images/sec", "value": None, "unit": "images/s",
+                                               "n_gpus": args.gpus, "dp_error": "CommFailure: %s" % e})
+                                   + "\n").encode())
+            sys.stderr.flush()
+            os._exit(3)
+        raise
 
+
+def run(args, json_fd):
     from sqr import dist
     rank, world = dist.env()[:2]
+    cuda = args.device == "cuda"
     try:
-        rank, world, dev = dist.init("nccl")
+        if cuda:
+            rank, world, dev = dist.init("nccl")
+        else:
+            torch.set_num_threads(max(1, min(torch.get_num_threads(), cpu_quota() // max(1, world))))
+            rank, world, dev = dist.init("gloo", "cpu")
         dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype)
         tr = Trainer(dev, config=args.config, batch=args.batch, render=args.render, dtype=dtype,
-                     graph=args.graph != 0, rank=rank, world=world, dp_rehearsal=args.dp_rehearsal)
+                     graph=args.graph != 0 and cuda, rank=rank, world=world, dp_rehearsal=args.dp_rehearsal,
+                     dp_overlap=bool(args.dp_overlap))
         B, H, R = tr.B, tr.H, tr.R
         probe_clock = None
         if tr.use_graph and not args.profile:
@@ -446,9 +526,13 @@ def main():
                                            "n_gpus": world, "dp_error": "%s: %s" % (type(e).__name__, e)})
                                + "\n").encode())
         raise
+    if rank == 0:
+        print("bench: rank 0 of %d ready (%s), %d warm-up + %d timed steps" % (
+            world, "graph" if tr.graph is not None else "eager", args.warmup, args.steps), file=sys.stderr, flush=True)
 
-    # dist.barrier: every rank's GPU work drained, then a host (gloo) barrier — no eager collective
-    # ever runs on the RCCL communicator that the captured step's all-reduces use
+    # dist.barrier: every rank's GPU work drained (with a deadline and the communicator's health
+    # check), then a host (gloo) barrier — no eager collective ever runs on the RCCL communicator
+    # that the captured step's all-reduces use
     for _ in range(args.warmup):
         tr.step()
     dist.barrier()
@@ -456,40 +540,48 @@ def main():
     for _ in range(args.steps):
         loss = tr.step()
     dist.barrier()
-    dt = time.perf_counter() - t0
-    dt = dist.max_over_ranks(dt)
+    dt_rank = time.perf_counter() - t0
+    dt = dist.max_over_ranks(dt_rank)
+    per_rank_ms = [v / args.steps * 1e3 for v in dist.gather_over_ranks(dt_rank)]
     final_loss = loss.item()
     value = B * world * args.steps / dt
-    dname = {torch.bfloat16: "bf16", torch.float16: "fp16"}[tr.dtype]
+    dname = {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}[tr.dtype]
 
     workload = {2: "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
                 3: "ResNetSQ + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam, data parallel" % R,
                 4: "ResNetSQ + ExplicitLoss(R=32)(labels) + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam" % R,
                 5: "ResNetSQ at 512x512 + ImplicitLoss(R=%d, tau=1.5, s=260) train step, Adam, %s%s"
                    % (R, dname, " + dynamic loss scaling" if tr.scaler is not None else "")}[args.config]
+    c = dist.comm()
     out = {"metric": "training images/sec (%dx%d depth, %s loss)" % (H, H, "explicit+implicit" if tr.crit_x else "implicit"),
            "value": value, "unit": "images/s",
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dname,
-           "data": "synthetic (GPU-rendered SQ depth images, reference label distribution)",
+           "data": "synthetic (%s-rendered SQ depth images, reference label distribution)" % ("GPU" if cuda else "host"),
            "config": {"workload": workload, "baseline_config": args.config,
                       "model": "ResNetSQ (resnet18 backbone, 11.37M params)", "global_batch": B * world,
                       "per_gpu_batch": B, "image": "%dx%dx1" % (H, H), "render_size": R,
                       "parallelism": "dp%d" % world},
-           "final_loss": final_loss, "hip_graph": tr.use_graph,
-           "dp": (("%s bucketed RCCL all-reduce on a side stream (libsqr communicator, RCCL %d)"
-                   % ("graph-captured" if tr.graph is not None else "eager", dist.comm().version))
-                  if tr.gdp is not None and dist.comm() is not None else None)}
+           "final_loss": final_loss, "hip_graph": tr.graph is not None,
+           "ms_per_step_per_rank": per_rank_ms,
+           "comm_world": c.world if c is not None else None,
+           "dp": (("%s %s (libsqr RCCL communicator, RCCL %d, %d ranks)"
+                   % ("graph-captured" if tr.graph is not None else "eager", tr.gdp.mode, c.version, c.world))
+                  if tr.gdp is not None and c is not None else
+                  ("eager %s over gloo" % tr.gdp.mode if tr.gdp is not None else None))}
+    if not cuda:
+        out["device"] = "cpu (host path over gloo: plumbing, not a throughput claim)"
     if tr.scaler is not None:
         out["loss_scale"] = float(tr.scaler.get_scale())
 
-    if not args.profile:
+    if not args.profile and cuda:
         kern_ms, nlaunch, how = time_probe(tr)
         flops = tr.probe_flops()
         achieved = flops / (kern_ms * 1e-3) / 1e12 if nlaunch else None
         ph = tr.probe_key()[3]
-        kname = "conv_%s %dx%d 3x3 s1 64->64 (layer1 %s direct conv, %s)" % (
-            PROBE[0], ph, ph, "persistent" if ph == 64 else "tiled", dname)
+        # the persistent layer-1 kernel runs both the 64-wide (256^2 input) and the 128-wide (512^2)
+        # maps (sqr_conv3.hip conv3p_kernel, one workgroup per CU over bands of row tiles)
+        kname = "conv_%s %dx%d 3x3 s1 64->64 (layer1 persistent direct conv, %s)" % (PROBE[0], ph, ph, dname)
         # algorithmic HBM bytes: the input read once and the output written once (16-bit; the 72-KiB
         # weight tensor is negligible).  This shape sits at the ridge point: at the peaks the MFMA
         # work takes flops / 2.5 PF and the bytes / 8 TB/s slightly longer, so the binding roof is

@@ -485,7 +485,9 @@ int sqr_tail_bwd(const sqr_tail_desc* t, const float* save, const sqr_tail_grads
  *   sqr_comm_allreduce_sum_f32  in-place sum of count floats over the ranks;
  *   sqr_comm_broadcast   in-place byte broadcast from root (parameter / buffer init);
  *   sqr_comm_async_error 0, or the communicator's asynchronous failure as an error;
- *   sqr_comm_destroy     finalize + destroy (after every graph holding its collectives is destroyed).
+ *   sqr_comm_destroy     finalize + destroy (after every graph holding its collectives is destroyed);
+ *   sqr_comm_abort       ncclCommAbort + free: a rank whose host deadline expired or whose peer failed
+ *                        (sqr.dist.wait_device) releases its in-flight collectives and exits.
  * Errors from RCCL are returned as 1000 + ncclResult_t. */
 #define SQR_COMM_ID_BYTES 128
 typedef struct sqr_comm* sqr_comm_t;
@@ -496,6 +498,7 @@ int sqr_comm_allreduce_sum_f32(sqr_comm_t comm, float* buf, size_t count, void* 
 int sqr_comm_broadcast(sqr_comm_t comm, void* buf, size_t bytes, int root, void* stream);
 int sqr_comm_async_error(sqr_comm_t comm);
 int sqr_comm_destroy(sqr_comm_t comm);
+int sqr_comm_abort(sqr_comm_t comm);
 
 #ifdef __cplusplus
 }

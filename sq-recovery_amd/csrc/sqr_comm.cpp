@@ -30,6 +30,7 @@ struct Rccl {
   ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*comm_finalize)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
   ncclResult_t (*comm_async_error)(ncclComm_t, ncclResult_t*) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   ncclResult_t (*get_version)(int*) = nullptr;
@@ -58,7 +59,8 @@ int load_rccl(const char* path) {
   r.handle = h;
   bool ok = bind(h, "ncclGetUniqueId", &r.get_unique_id) && bind(h, "ncclCommInitRank", &r.comm_init_rank) &&
             bind(h, "ncclAllReduce", &r.all_reduce) && bind(h, "ncclBroadcast", &r.broadcast) &&
-            bind(h, "ncclCommDestroy", &r.comm_destroy) && bind(h, "ncclGetErrorString", &r.error_string) &&
+            bind(h, "ncclCommDestroy", &r.comm_destroy) &&
+            bind(h, "ncclCommAbort", &r.comm_abort) && bind(h, "ncclGetErrorString", &r.error_string) &&
             bind(h, "ncclCommGetAsyncError", &r.comm_async_error) && bind(h, "ncclGetVersion", &r.get_version);
   if (!ok) {
     sqr::set_error("comm: %s lacks an RCCL entry point", p);
@@ -163,4 +165,15 @@ extern "C" int sqr_comm_destroy(sqr_comm_t comm) {
   if (r != ncclSuccess && rc == 0) rc = rccl_fail("ncclCommDestroy", r);
   delete comm;
   return rc;
+}
+
+// A rank that gives up (host deadline expired, a peer reported an error): ncclCommAbort stops the
+// communicator's in-flight kernels and proxy thread instead of waiting for peers that may be gone.
+extern "C" int sqr_comm_abort(sqr_comm_t comm) {
+  if (!comm) return 0;
+  SQR_RCCL_LOADED();
+  ncclResult_t r = g_rccl.comm_abort(comm->nc);
+  delete comm;
+  if (r != ncclSuccess) return rccl_fail("ncclCommAbort", r);
+  return 0;
 }

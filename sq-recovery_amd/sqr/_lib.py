@@ -185,6 +185,7 @@ SIGNATURES = {
     "sqr_comm_broadcast": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "sqr_comm_async_error": (c_int, [c_void_p]),
     "sqr_comm_destroy": (c_int, [c_void_p]),
+    "sqr_comm_abort": (c_int, [c_void_p]),
 }
 
 

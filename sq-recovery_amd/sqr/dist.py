@@ -15,8 +15,11 @@ statistics (the reference trains on one GPU; DDP without SyncBN is the documente
 semantics: an N-rank step equals the average of N independent per-rank gradients).
 """
 import ctypes
+import datetime
 import gc
 import os
+import sys
+import time
 
 import torch
 import torch.distributed as dist
@@ -25,6 +28,18 @@ import torch.distributed as dist
 # all-reduce runs near xGMI link bandwidth, small enough that the first bucket (layer4 + heads)
 # starts while layer3..layer1 backward still runs.
 BUCKET_MB = 16
+
+# Host-side deadlines (no ProcessGroupNCCL watchdog watches libsqr's communicator, so the host does):
+# the gloo group's collectives (unique-id exchange, barriers, timing reductions) and every wait for
+# device work that may hold RCCL kernels (wait_event).  A rank whose peer died would otherwise block
+# forever inside a captured all-reduce.
+HOST_TIMEOUT_S = float(os.environ.get("SQR_HOST_TIMEOUT_S", "900"))
+DEVICE_TIMEOUT_S = float(os.environ.get("SQR_DEVICE_TIMEOUT_S", "600"))
+
+
+class CommFailure(RuntimeError):
+    """The data path gave up: a device wait passed its deadline or the communicator reported an
+    asynchronous error.  The communicator has been aborted (ncclCommAbort) when this is raised."""
 
 
 def env():
@@ -95,6 +110,9 @@ class Comm:
         a broken communicator fails here, loudly, not inside a replayed graph."""
         t = torch.full((1024,), float(self.rank + 1), dtype=torch.float32, device=device)
         self.allreduce_(t)
+        ev = torch.cuda.Event()
+        ev.record()
+        wait_event(ev, what="communicator self-test", comm_=self)
         torch.cuda.synchronize(device)
         self.check()
         want = self.world * (self.world + 1) / 2
@@ -106,6 +124,13 @@ class Comm:
         h, self.handle = self.handle, None
         if h is not None:
             check(lib().sqr_comm_destroy(h), "sqr_comm_destroy")
+
+    def abort(self):
+        """ncclCommAbort: stop this rank's in-flight collectives without waiting for the peers."""
+        from ._lib import lib
+        h, self.handle = self.handle, None
+        if h is not None:
+            lib().sqr_comm_abort(h)
 
 
 _comm = [None]
@@ -148,7 +173,7 @@ def init(backend="nccl", device_type=None):
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=HOST_TIMEOUT_S))
     if world > 1 and backend == "nccl" and device.type == "cuda":
         open_comm(device, rank, world)
     return rank, world, device
@@ -184,13 +209,19 @@ class GraphDataParallel:
     broadcast from rank 0 once, BatchNorm statistics stay per rank.  Gradients must be None before
     each backward (``optimizer.zero_grad(set_to_none=True)``; checked)."""
 
-    def __init__(self, model, optimizer, device, bucket_mb=BUCKET_MB):
+    def __init__(self, model, optimizer, device, bucket_mb=BUCKET_MB, overlap=True, comm_=None):
+        """overlap=False: one all-reduce of the whole flat buffer after the backward, on the compute
+        stream (no side stream, no hooks-driven launches) — the fallback to read an N-GPU curve
+        against when the overlapped buckets slow the backward kernels they run beside.  comm_: the
+        communicator to use instead of this process's (tests drive the N>1 branches with a stand-in
+        over gloo)."""
         from . import gradbuf
         self.model = model
         device = torch.device(device)
+        self.overlap = bool(overlap)
         # the RCCL communicator when this process has one (CUDA, one GPU per rank), else the
         # process group (gloo: the host path, or several ranks sharing one GPU)
-        self.comm = comm() if device.type == "cuda" else None
+        self.comm = comm_ if comm_ is not None else (comm() if device.type == "cuda" else None)
         self.world = self.comm.world if self.comm is not None else (
             dist.get_world_size() if dist.is_initialized() else 1)
         self.params = [p for p in model.parameters() if p.requires_grad]
@@ -204,9 +235,9 @@ class GraphDataParallel:
         order = list(reversed(self.params))  # the backward produces the last layers' grads first
         self.flat = gradbuf.install(order, device)
         self.param_of = {id(p): p for p in self.params}
-        # buckets: contiguous ranges of the flat buffer
+        # buckets: contiguous ranges of the flat buffer (one bucket without overlap)
         self.buckets, self.bucket_of, start, members = [], {}, 0, []
-        cap = int(bucket_mb * 2 ** 20 / 4)
+        cap = int(bucket_mb * 2 ** 20 / 4) if self.overlap else self.flat.numel() + 1
         off = 0
         for p in order:
             members.append(id(p))
@@ -219,7 +250,7 @@ class GraphDataParallel:
         for b, (_, _, mem) in enumerate(self.buckets):
             for pid in mem:
                 self.bucket_of[pid] = b
-        self.side = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self.side = torch.cuda.Stream(device) if (device.type == "cuda" and self.overlap) else None
         self.launch_log = []  # bucket indices in launch order (tests)
         self._reset()
         gradbuf.set_listener(self._written)
@@ -229,6 +260,10 @@ class GraphDataParallel:
         self.fused_scale = hasattr(optimizer, "sqr_grad_scale") and device.type == "cuda"
         if self.fused_scale:
             optimizer.sqr_grad_scale = 1.0 / self.world
+
+    @property
+    def mode(self):
+        return "overlapped buckets" if self.overlap else "one post-backward all-reduce"
 
     def _reset(self):
         self.pending = [len(mem) for _, _, mem in self.buckets]
@@ -244,15 +279,19 @@ class GraphDataParallel:
             return
         lo, hi, _ = self.buckets[b]
         view = self.flat[lo:hi]
-        if self.side is None:
-            dist.all_reduce(view)
+        if self.side is not None:
+            # overlapped: fork to the side stream after the gradients queued so far
+            self.side.wait_stream(torch.cuda.current_stream())
+            if self.comm is not None:
+                self.comm.allreduce_(view, self.side)  # SUM in place; the optimizer scales by 1 / world
+                return
+            with torch.cuda.stream(self.side):
+                dist.all_reduce(view)
             return
-        self.side.wait_stream(torch.cuda.current_stream())
         if self.comm is not None:
-            self.comm.allreduce_(view, self.side)  # SUM in place; the optimizer scales by 1 / world
+            self.comm.allreduce_(view)  # in line, on the current (compute) stream
             return
-        with torch.cuda.stream(self.side):
-            dist.all_reduce(view)
+        dist.all_reduce(view)
 
     def _mark(self, pid):
         if pid in self.done:
@@ -262,7 +301,7 @@ class GraphDataParallel:
         if b is None:
             return
         self.pending[b] -= 1
-        if self.pending[b] == 0:
+        if self.pending[b] == 0 and self.overlap:
             self._launch(b)
 
     def _check_cleared(self, _module, _inputs):
@@ -348,6 +387,16 @@ def max_over_ranks(x):
     return t.item()
 
 
+def gather_over_ranks(x):
+    """[x of rank 0, x of rank 1, ...] (host floats over the host group)."""
+    if not _multi():
+        return [float(x)]
+    t = torch.zeros(dist.get_world_size(), dtype=torch.float64)
+    t[dist.get_rank()] = float(x)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=host_group())
+    return t.tolist()
+
+
 def mean_over_ranks(x):
     if not _multi():
         return float(x)
@@ -356,11 +405,64 @@ def mean_over_ranks(x):
     return t.item() / dist.get_world_size()
 
 
-def barrier():
-    """Every rank's queued GPU work has finished, then a host barrier (gloo): the bench's timed
-    region starts and ends with all devices idle."""
-    if _cuda_live():
+def _give_up(why, c):
+    """Abort communicator c (its kernels stop waiting for peers) and raise CommFailure."""
+    if _comm[0] is c:
+        _comm[0] = None
+    if c is not None:
+        try:
+            c.abort()
+        except Exception as e:  # the failure being reported matters more
+            print("sqr.dist: ncclCommAbort failed: %s" % e, file=sys.stderr, flush=True)
+    raise CommFailure(why)
+
+
+def wait_event(ev, timeout=None, what="device work", comm_=None):
+    """ev.synchronize() with a deadline and the communicator's health check: poll the event
+    (hipEventQuery), and every 50 ms ask the communicator for an asynchronous error.  On a timeout
+    or an error the communicator is aborted and CommFailure raised, so no rank blocks forever in
+    an all-reduce whose peer is gone.  Without a multi-rank communicator: ev.synchronize()."""
+    c = comm_ or _comm[0]
+    if c is None or c.world == 1:
+        ev.synchronize()
+        return
+    timeout = DEVICE_TIMEOUT_S if timeout is None else timeout
+    t0 = time.monotonic()
+    next_check, n = t0, 0
+    while not ev.query():
+        n += 1
+        now = time.monotonic()
+        if now >= next_check:
+            try:
+                c.check()
+            except Exception as e:
+                _give_up("%s: communicator error while waiting: %s" % (what, e), c)
+            next_check = now + 0.05
+        if now - t0 > timeout:
+            _give_up("%s did not finish within %.0f s (a peer rank stalled or died?)" % (what, timeout), c)
+        if n > 2000:  # after the first ~ms of spinning, yield between polls
+            time.sleep(1e-4)
+
+
+def wait_device(timeout=None, what="device work"):
+    """All work queued on the current stream (and every stream joined into it) has finished:
+    torch.cuda.synchronize() for a single rank, wait_event() under a multi-rank communicator."""
+    if not _cuda_live():
+        return
+    c = _comm[0]
+    if c is None or c.world == 1:
         torch.cuda.synchronize()
+        return
+    ev = torch.cuda.Event()
+    ev.record()
+    wait_event(ev, timeout, what)
+    torch.cuda.synchronize()  # finished already; also covers streams not joined into this one
+
+
+def barrier():
+    """Every rank's queued GPU work has finished (with a deadline, wait_device), then a host
+    barrier (gloo): the bench's timed region starts and ends with all devices idle."""
+    wait_device(what="barrier")
     if _multi():
         dist.barrier(group=host_group())
 
@@ -370,8 +472,7 @@ def finish(*graphs):
     are released with the graph, and must be before their communicator goes); drain again; wait for
     every rank on the host group; destroy the RCCL communicator; wait again; only then destroy the
     process group."""
-    if _cuda_live():
-        torch.cuda.synchronize()
+    wait_device(what="teardown")
     for g in graphs:
         if g is not None:
             g.reset()

@@ -113,7 +113,8 @@ class CapturedStep:
             slot = self.read % RING
             ev = self.events[slot]
             if ev is not None:
-                ev.synchronize()
+                from . import dist
+                dist.wait_event(ev, what="training step %d" % self.read)  # deadline + RCCL health
             out.append((float(self.host[slot, 0]), bool(self.host[slot, 1] != 0)))
             self.read += 1
         return out

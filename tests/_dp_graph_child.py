@@ -4,7 +4,8 @@ teardown (sqr.dist.finish: drain, destroy the step graphs with their captured al
 communicator) and a normal interpreter exit.
 
   A. GraphDataParallel eagerly equals plain training bitwise; the step with its all-reduce captured
-     in one HIP graph and replayed follows the same parameter trajectory;
+     in one HIP graph and replayed follows the same parameter trajectory — with overlapped bucket
+     all-reduces (default) and with one post-backward all-reduce (bench.py --dp-overlap 0);
   B. sqr.step.CapturedStep (train.py's stepper) over GraphDataParallel through full batches, a
      partial batch (eager all-reduces between graph replays) and a learning-rate change (recapture:
      the old graph drained and destroyed first): per-step losses and NaN flags equal the eager loop;
@@ -89,36 +90,38 @@ def run(tmp_path):
         rng = np.random.default_rng(0)
         p = torch.tensor(classes.sample_sq_params(rng, 8), device=DEV)
         x = losses.implicit_render(p, 256, 1.5, 260).unsqueeze(1).contiguous()
-        a_net, a_opt, a_crit = _setup()
-        b_net, b_opt, b_crit = _setup()
-        gdp = sdist.GraphDataParallel(b_net, b_opt, DEV)
-        assert gdp.comm is comm
-        for _ in range(2):
-            a_opt.zero_grad(set_to_none=True)
+        # both all-reduce modes: overlapped buckets on a side stream, one post-backward all-reduce
+        for overlap in (True, False):
+            a_net, a_opt, a_crit = _setup()
+            b_net, b_opt, b_crit = _setup()
+            gdp = sdist.GraphDataParallel(b_net, b_opt, DEV, overlap=overlap)
+            assert gdp.comm is comm and len(gdp.buckets) == (3 if overlap else 1)
+            for _ in range(2):
+                a_opt.zero_grad(set_to_none=True)
+                b_opt.zero_grad(set_to_none=True)
+                la = _body(a_net, a_opt, a_crit, x)
+                lb = _body(b_net, b_opt, b_crit, x, gdp)
+                gdp.check_grads()
+                assert torch.equal(la, lb)
+            for pa, pb in zip(a_net.parameters(), b_net.parameters()):
+                assert torch.equal(pa, pb)
+            # capture the DP step (all-reduce included) and replay it
+            g = torch.cuda.CUDAGraph()
+            graphs.append(g)
             b_opt.zero_grad(set_to_none=True)
-            la = _body(a_net, a_opt, a_crit, x)
-            lb = _body(b_net, b_opt, b_crit, x, gdp)
-            gdp.check_grads()
-            assert torch.equal(la, lb)
-        for pa, pb in zip(a_net.parameters(), b_net.parameters()):
-            assert torch.equal(pa, pb)
-        # capture the DP step (all-reduce included) and replay it
-        g = torch.cuda.CUDAGraph()
-        graphs.append(g)
-        b_opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            static = _body(b_net, b_opt, b_crit, x, gdp)
-        for _ in range(2):
-            g.replay()
-            a_opt.zero_grad(set_to_none=True)
-            la = _body(a_net, a_opt, a_crit, x)
-            torch.cuda.synchronize()
-            assert abs(la.item() - static.item()) <= 1e-6 * abs(la.item())
-        for pa, pb in zip(a_net.parameters(), b_net.parameters()):
-            assert (pa - pb).abs().max().item() <= 1e-5 * max(pa.abs().max().item(), 1e-3)
-        comm.check()
-        gdp.close(b_opt)
-        gdp = None
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                static = _body(b_net, b_opt, b_crit, x, gdp)
+            for _ in range(2):
+                g.replay()
+                a_opt.zero_grad(set_to_none=True)
+                la = _body(a_net, a_opt, a_crit, x)
+                torch.cuda.synchronize()
+                assert abs(la.item() - static.item()) <= 1e-6 * abs(la.item())
+            for pa, pb in zip(a_net.parameters(), b_net.parameters()):
+                assert (pa - pb).abs().max().item() <= 1e-5 * max(pa.abs().max().item(), 1e-3)
+            comm.check()
+            gdp.close(b_opt)
+            gdp = None
         print("DP_GRAPH_OK", flush=True)
 
         # B: the stepper: 3 full batches, a partial one, an LR change (recapture), 2 more full ones

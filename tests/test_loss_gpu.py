@@ -67,6 +67,29 @@ def test_implicit_vs_oracle_sizes(R):
     _grad_close(g, G)
 
 
+@pytest.mark.parametrize("R,tau", [(64, 1.5), (64, 6.0), (64, 12.0), (128, 6.0)])
+def test_implicit_grad_prefix_form_vs_f64(R, tau):
+    """The kernel's 17 gradient moments use suffix sums of the transmittance as Ttot - prefix
+    (one pass down each ray, sqr_loss.hip).  Its fp32 error is ~eps * Ttot per term, Ttot <= R, and
+    it matters most where the true suffix is small: a large tau (the transmittance dies inside the
+    object) and long rays.  Against the float64 two-pass oracle (oracle/sq_oracle.py, the
+    reference's autograd of classes.py:284-291), the parameter gradient stays within
+    2e-4 + 8 * R * eps32 of max|g_ref| per sample."""
+    rng = np.random.default_rng(int(R * 10 + tau))
+    B = 4
+    pred = _sample(rng, B)
+    from sqr import losses
+    # targets rendered from nearby parameters: the silhouettes overlap, so the gradient is not
+    # dominated by the background pixels
+    near = pred.copy()
+    near[:, :8] = np.clip(pred[:, :8] + rng.normal(scale=0.02, size=(B, 8)), 0.02, 0.98)
+    true = losses.implicit_render(torch.tensor(near, device=DEV), 256, tau, 260).unsqueeze(1).cpu().numpy()
+    L, G, _, _ = O.implicit_loss(true, pred, R, tau, 260)
+    loss, g = _run_implicit(true, pred, R, tau, 260)
+    assert abs(loss.item() - L) <= 1e-4 * abs(L)
+    _grad_close(g, G, rel=2e-4 + 8 * R * 2.0 ** -23)
+
+
 def test_implicit_render_matches_oracle():
     from sqr import losses
     rng = np.random.default_rng(3)

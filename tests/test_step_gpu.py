@@ -8,8 +8,10 @@ step on the same images and the same 16-bit-rounded conv weights.  The tolerance
 guessed: a CPU float32 run that rounds to the compute dtype at the GPU step's storage points (conv
 operands and outputs, BatchNorm / pooled activations, and - through autograd of the casts - the
 activation gradients) measures how far a correct 16-bit step lands from float64; the GPU step must
-land as close (L2 error x4 per parameter and x1.6 as the geometric mean over all parameters, max
-error x5, with a small absolute floor for parameters whose gradient is ~0).
+land as close (L2 error x3 per parameter and x1.6 as the geometric mean over all parameters, max
+error x5, with a small absolute floor for parameters whose gradient is ~0).  Every config runs at
+the bench batch (64): the head-bias gradients are sums over the batch's predictions, and at 16
+images one chaotic bf16 draw could dominate them (round 4 measured a 3.4x head-bias ratio at B=16).
 """
 import os
 
@@ -88,8 +90,8 @@ def _fix_tail(model, masks):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("config,batch,dtype", [(2, 64, None), (4, 64, None), (5, 16, None), (5, 16, torch.bfloat16)],
-                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B16", "cfg5shape_bf16_512_B16"])
+@pytest.mark.parametrize("config,batch,dtype", [(2, 64, None), (4, 64, None), (5, 64, None), (5, 64, torch.bfloat16)],
+                         ids=["cfg2_bf16_B64", "cfg4_bf16_B64", "cfg5_fp16_512_B64", "cfg5shape_bf16_512_B64"])
 def test_bench_step_gradients_vs_f64(config, batch, dtype):
     import bench
     import ref_torch
@@ -134,17 +136,12 @@ def test_bench_step_gradients_vs_f64(config, batch, dtype):
         h.remove()
 
     assert abs(loss_gpu - loss64) <= max(3 * abs(loss_emu - loss64), 1e-4 * abs(loss64)), (loss_gpu, loss_emu, loss64)
-    # Two error measures per parameter, each against the emulation's: the L2-relative error and the
-    # max-abs relative error (x5), plus the geometric mean of the L2 ratios over all parameters
+    # Two error measures per parameter, each against the emulation's: the L2-relative error (x3) and
+    # the max-abs relative error (x5), plus the geometric mean of the L2 ratios over all parameters
     # (<= 1.6: a systematic error moves many parameters at once, noise does not).  A ReLU input
     # within rounding distance of 0 takes either branch in a correct 16-bit step; one such element
     # moves one channel of a BatchNorm gradient, so the per-channel maximum is heavy-tailed
-    # (measured: cfg5 fp16 B=16 layer4.0.bn1.bias max ratio 3.7 with L2 ratio 1.1).  The per-
-    # parameter L2 ratio of a correct step is heavy-tailed too at bf16 with 16 images: the head
-    # biases' gradients are sums over 16 predictions, each a chaotic function of the bf16 forward
-    # (measured, cfg5 bf16 B=16, data seeds 1234/1/2/3, the tiled layer-1 kernel and the persistent
-    # one — each against float64 in tests/test_conv_gpu.py: worst ratios 1.2 / 1.6 / 2.2 / 1.2 and
-    # 3.4 / 2.1 / 1.8 / 1.5, output_rotation.out_layer.0.bias at 3.4), hence x4.
+    # (measured: cfg5 fp16 B=16 layer4.0.bn1.bias max ratio 3.7 with L2 ratio 1.1) — hence x5 there.
     worst, logr = [], []
     for n, b in g64.items():
         e_gpu, e_emu = _rel_err(g_gpu[n], b), _rel_err(g_emu[n], b)
@@ -157,7 +154,7 @@ def test_bench_step_gradients_vs_f64(config, batch, dtype):
           "geometric mean L2 ratio %.3f" % gmean)
     assert gmean <= 1.6, gmean
     for _, n, l_gpu, l_emu, e_gpu, e_emu in worst:
-        assert l_gpu <= 4 * l_emu + 1e-3, (n, "l2", l_gpu, l_emu)
+        assert l_gpu <= 3 * l_emu + 1e-3, (n, "l2", l_gpu, l_emu)
         assert e_gpu <= 5 * e_emu + 1e-3, (n, "max", e_gpu, e_emu)
     # the step then applied Adam: every parameter moved, by at most ~lr (Adam's first-order bound)
     for n, p in tr.net.named_parameters():
