@@ -263,7 +263,7 @@ def time_loss_call(crit, images, B, dev, reps=20):
 
 # the probe kernel's forward instance in rocprofv3 kernel names (tools/traffic.py FWD_RE: the
 # statistics-producing conv3p_kernel<T, STATS=true, ACC=false, BNB=false>, mangled or demangled)
-_PROBE_RE = r"conv3p_kernel(IDF16b?Lb1ELb0ELb0ELi\d+ELi\d+ELb0E|<[^<>]*?,\s*true,\s*false,\s*false,\s*\d+,\s*\d+(,\s*false)?>|<bool _Accum, bool, E, false, false(, \d+, \d+(, false)?)?>)"
+_PROBE_RE = r"conv3p_kernel(IDF16[b_]?Lb1ELb0ELb0ELi\d+ELi\d+ELb0E|<[^<>]*?,\s*true,\s*false,\s*false,\s*\d+,\s*\d+(,\s*false)?>|<bool _Accum, bool, E, false, false(, \d+, \d+(, false)?)?>)"
 
 
 def kernel_src_sha():
@@ -282,15 +282,25 @@ def kernel_src_sha():
     return h.hexdigest()[:16]
 
 
+def pmc_suffix(H, dname):
+    """Which committed PMC summary describes this run's step: "" = the default config-2 step (256x256,
+    bf16: profiles/pmc_step.json, traffic.json), "_c5" = config 5 (512x512, fp16: pmc_step_c5.json,
+    traffic_c5.json); None = no summary collected for this shape / dtype."""
+    return {(256, "bf16"): "", (512, "fp16"): "_c5"}.get((H, dname))
+
+
 def pmc_summary(H, dname):
     """MFMA-busy and issue counters of the step's kernels from the committed rocprofv3 PMC summary
-    (profiles/pmc_step.json, written by tools/pmc_step.py from tools/gpu_pmc_step.sh on the default
-    config-2 step): the probe kernel's counters and the step-wide MFMA utilisation (MFMA-busy cycles of
-    every kernel over every kernel's duration x 1024 SIMDs).  Counters collected on other kernel
-    sources than the ones built here (src_sha) are not reported: only the staleness is."""
+    (profiles/pmc_step{,_c5}.json, written by tools/pmc_step.py from tools/gpu_pmc_step.sh on the
+    config-2 / config-5 step): the probe kernel's counters and the step-wide MFMA utilisation
+    (MFMA-busy cycles of every kernel over every kernel's duration x 1024 SIMDs).  Counters collected
+    on other kernel sources than the ones built here (src_sha) are not reported: only the staleness is."""
     import re
-    path = os.path.join(ROOT, "profiles", "pmc_step.json")
-    if not os.path.exists(path) or H != 256 or dname != "bf16":
+    suf = pmc_suffix(H, dname)
+    if suf is None:
+        return None
+    path = os.path.join(ROOT, "profiles", "pmc_step%s.json" % suf)
+    if not os.path.exists(path):
         return None
     with open(path) as f:
         data = json.load(f)
@@ -298,8 +308,8 @@ def pmc_summary(H, dname):
     cur = kernel_src_sha()
     if sha != cur:
         return {"stale": True, "collected_src_sha": sha, "current_src_sha": cur,
-                "source": "profiles/pmc_step.json (collected on other kernel sources: counters omitted)"}
-    out = {"source": "profiles/pmc_step.json (rocprofv3 --pmc, eager step, mean per dispatch)", "src_sha": sha}
+                "source": "profiles/pmc_step%s.json (collected on other kernel sources: counters omitted)" % suf}
+    out = {"source": "profiles/pmc_step%s.json (rocprofv3 --pmc, eager step, mean per dispatch)" % suf, "src_sha": sha}
     probe = [r for r in rows if re.search(_PROBE_RE, r["kernel"])]
     if probe:
         r = probe[0]
@@ -597,11 +607,12 @@ def run(args, json_fd):
         roof = dict(hbm_view if t_hbm >= t_mfma else mfma_view)
         roof.update({"kernel_ms": kern_ms, "launches": nlaunch, "timing": how, "traffic": None,
                      "time_at_peak_us": {"mfma": t_mfma * 1e6, "hbm": t_hbm * 1e6}})
-        path = os.path.join(ROOT, "profiles", "traffic.json")
-        if os.path.exists(path):
+        suf = pmc_suffix(H, dname)
+        path = os.path.join(ROOT, "profiles", "traffic%s.json" % suf) if suf is not None else None
+        if path and os.path.exists(path):
             with open(path) as f:
                 trf = json.load(f)
-            if trf.get("kernel_key") == list(PROBE) and H == 256 and dname == "bf16":
+            if trf.get("kernel_key") == list(PROBE):
                 if trf.get("src_sha") == kernel_src_sha():
                     roof["traffic"] = trf.get("hbm_bytes_per_launch")
                 else:  # measured on other kernel sources: not this build's traffic

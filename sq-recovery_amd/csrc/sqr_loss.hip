@@ -24,6 +24,7 @@
 // the closed-form chain through u = Rc (g - t)/a, the quaternion and the clamp masks.
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 #include "sqr_common.h"
 
 namespace sqr {
@@ -186,16 +187,6 @@ __device__ __forceinline__ void vox_bwd(const SQ& s, const Vox& f, float occ, fl
   M.m[16] = fmaf(gu2, gz, M.m[16]);
 }
 
-// dL/docc = 1 at one voxel: its 17 parameter moments J (vox_bwd is gocc * J)
-__device__ __forceinline__ void vox_jac(const SQ& s, const Vox& f, float occ, float omo, float sharp, float gx,
-                                        float gy, float gz, float* J) {
-  Moments M;
-  M.zero();
-  vox_bwd(s, f, occ, omo, 1.f, sharp, gx, gy, gz, M);
-#pragma unroll
-  for (int i = 0; i < 17; ++i) J[i] = M.m[i];
-}
-
 // block-wide sum of kNAcc floats -> out (thread 0..kNAcc-1 write)
 template <int NT>
 __device__ __forceinline__ void block_reduce_store(float* vals, float* red, float* out) {
@@ -214,6 +205,46 @@ __device__ __forceinline__ void block_reduce_store(float* vals, float* red, floa
   }
 }
 
+// dL/docc = 1 at one voxel: the 11 moments of its Jacobian that vary along a ray, J[0..10] =
+// (m0..m7, m10, m13, m16): gx and gy are constant along a ray, so m8 = gx m5, m9 = gy m5,
+// m11 = gx m6, m12 = gy m6, m14 = gx m7, m15 = gy m7 are formed once per ray (ray_moments)
+__device__ __forceinline__ void vox_jac11(const SQ& s, const Vox& f, float occ, float omo, float sharp, float gz,
+                                          float* J) {
+  const float hG = -sharp * occ * omo * f.G;  // dL/dln G at dL/docc = 1
+  const float g_lnF = hG * s.e1;
+  const float g_lnE = g_lnF * f.rE;
+  const float g_lnC = g_lnF * f.rC;
+  const float g_lnF1 = g_lnE * s.r21;
+  const float g_lnA = g_lnF1 * f.rA, g_lnB = g_lnF1 * f.rB;
+  J[3] = kLn2 * (hG * f.lF - (g_lnE * f.lE + g_lnC * f.lC) * s.ie1);
+  J[4] = kLn2 * s.ie2 * (g_lnE * f.lE - g_lnA * f.lA - g_lnB * f.lB);
+  // d lnA1/du0 = 2 u0 / A1: the share times 2^-log2(A1) (A1 itself may sit below FLT_MIN)
+  const float gu0 = 2.f * f.u0 * s.ie2 * g_lnA * fexp2(-f.lA1);
+  const float gu1 = 2.f * f.u1 * s.ie2 * g_lnB * fexp2(-f.lB1);
+  const float gu2 = 2.f * f.u2 * s.ie1 * g_lnC * fexp2(-f.lC1);
+  J[0] = gu0 * f.u0;
+  J[1] = gu1 * f.u1;
+  J[2] = gu2 * f.u2;
+  J[5] = gu0;
+  J[6] = gu1;
+  J[7] = gu2;
+  J[8] = gu0 * gz;
+  J[9] = gu1 * gz;
+  J[10] = gu2 * gz;
+}
+
+// the 17 moments of a ray from its 11 accumulated ones (v: [0..7] = m0..m7, [8..10] = m10, m13, m16)
+__device__ __forceinline__ void ray_moments(const float* v, float gx, float gy, float* out) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = v[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    out[8 + 3 * i] = gx * v[5 + i];
+    out[9 + 3 * i] = gy * v[5 + i];
+    out[10 + 3 * i] = v[8 + i];
+  }
+}
+
 // -------------------------------------------------------------------------- ImplicitLoss
 // grid: (blocks_per_sample, B); one thread per output pixel (ray), walking it ONCE, top-down
 // (flipped z, classes.py:277).
@@ -222,15 +253,18 @@ __device__ __forceinline__ void block_reduce_store(float* vals, float* red, floa
 // moments at dL/docc = 1).  With suffix_m = Ttot - P_{m-1} (P the exclusive prefix of T),
 // M = cg (Ttot * sum J - sum P_{m-1} J_m): both sums accumulate on the way down, so the voxel chain
 // is evaluated once (round 3's second, bottom-up pass recomputed it for the suffix sums: 28 instead
-// of 18 transcendentals per voxel, T kept in LDS; B = 64 call 31 -> 27 us at R = 32, kernel 97 -> 85
-// us at R = 64).  The subtraction cancels where the suffix is small next to Ttot (behind the
-// surface, where J is small too): relative error ~ eps * Ttot / suffix.  (Splitting a ray over 4
-// lanes, segment transmittances combined by lane scans, measured slower: 32 / 121 us.)
+// of 18 transcendentals per voxel, T kept in LDS).  The subtraction cancels where the suffix is
+// small next to Ttot (behind the surface, where J is small too): relative error ~ eps * Ttot /
+// suffix (tests/test_loss_gpu.py::test_implicit_grad_prefix_form_vs_f64 bounds it at R = 64, 128 and
+// tau up to 12).
+// Per voxel only the 11 moments that vary along the ray accumulate (vox_jac11).
+// The target pixel is loaded before the walk, its latency hidden behind it.
 // dyn LDS: axis[R] + reduction scratch.
 template <int NT, bool NEED_GRAD, int UNR = 1>
 __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     const float* __restrict__ params, const float* __restrict__ target, int H, int W, int R,
     float tau, float sharp, float* __restrict__ partials) {
+  constexpr int NM = NEED_GRAD ? 11 : 1;
   extern __shared__ float lds[];
   float* axis = lds;                           // [R]
   float* red = axis + ((R + 3) & ~3);          // [NT/64][kNAcc]
@@ -240,23 +274,32 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     axis[i] = (i == 0) ? 1e-4f : (R > 1 ? (float)i / (float)(R - 1) : 1e-4f);
   SQ s;
   sq_load(params + 12 * b, s);
-  __syncthreads();
 
   const int pix = blockIdx.x * NT + threadIdx.x;
   const bool active = pix < R * R;
+  const int r = active ? pix / R : 0, c = active ? pix - r * R : 0;
+  // F.interpolate nearest (float scale, floor, clamp) — issued now, used after the walk
+  float tv = 0.f;
+  if (active) {
+    const float sh = (float)H / (float)R, sw = (float)W / (float)R;
+    const int sr = min((int)floorf((float)r * sh), H - 1);
+    const int sc = min((int)floorf((float)c * sw), W - 1);
+    tv = target[((size_t)b * H + sr) * W + sc];
+  }
+  __syncthreads();
+
   float vals[kNAcc];
 #pragma unroll
   for (int i = 0; i < kNAcc; ++i) vals[i] = 0.f;
-  if (active) {
-    const int r = pix / R, c = pix - r * R;
-    const int ix = c, iy = R - 1 - r;  // D[r,c] = depth[x=c, y=R-1-r] (classes.py:279)
-    const float gx = axis[ix], gy = axis[iy];
-    const float dx = gx - s.t[0], dy = gy - s.t[1];
-    float S = 0.f, P = 0.f;  // occupancy sum, prefix of T
-    float JA[NEED_GRAD ? 17 : 1], JB[NEED_GRAD ? 17 : 1];  // sum J, sum P_{m-1} J_m
+  const int ix = c, iy = R - 1 - r;  // D[r,c] = depth[x=c, y=R-1-r] (classes.py:279)
+  const float gx = axis[ix], gy = axis[iy];
+  const float dx = gx - s.t[0], dy = gy - s.t[1];
+  const float ntau = -tau * kLog2e;
+  float S = 0.f, P = 0.f;  // occupancy sum, prefix of T
+  float JA[NM], JB[NM];    // sum J, sum P_{m-1} J_m
 #pragma unroll
-    for (int i = 0; i < (NEED_GRAD ? 17 : 1); ++i) JA[i] = JB[i] = 0.f;
-    const float ntau = -tau * kLog2e;
+  for (int i = 0; i < NM; ++i) JA[i] = JB[i] = 0.f;
+  if (active) {
 #pragma unroll UNR
     for (int k = 0; k < R; ++k) {
       const float gz = axis[R - 1 - k];
@@ -267,29 +310,29 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
       S += occ;
       const float T = fexp2(ntau * S);
       if (NEED_GRAD) {
-        float J[17];
-        vox_jac(s, f, occ, omo, sharp, gx, gy, gz, J);
+        float J[11];
+        vox_jac11(s, f, occ, omo, sharp, gz, J);
 #pragma unroll
-        for (int i = 0; i < 17; ++i) {
+        for (int i = 0; i < NM; ++i) {
           JA[i] += J[i];
           JB[i] = fmaf(P, J[i], JB[i]);
         }
       }
       P += T;
     }
-    const float D = 1.f - P / (float)R;  // 1 - sum(T)/R (classes.py:278)
-    // F.interpolate nearest (float scale, floor, clamp)
-    const float sh = (float)H / (float)R, sw = (float)W / (float)R;
-    const int sr = min((int)floorf((float)r * sh), H - 1);
-    const int sc = min((int)floorf((float)c * sw), W - 1);
-    const float tv = target[((size_t)b * H + sr) * W + sc];
+  }
+  const float Ttot = P;
+  if (active) {
+    const float D = 1.f - Ttot / (float)R;  // 1 - sum(T)/R (classes.py:278)
     const float diff = D - tv;
     vals[17] = fabsf(diff);
     if (NEED_GRAD && diff != 0.f) {
       // dL/docc_m = sign(D-true) * tau/R * (Ttot - P_{m-1})   (scaled by 1/(B R^2) in finalize)
       const float cg = (diff > 0.f ? 1.f : -1.f) * tau / (float)R;
+      float v[NM];
 #pragma unroll
-      for (int i = 0; i < 17; ++i) vals[i] = cg * fmaf(P, JA[i], -JB[i]);
+      for (int i = 0; i < NM; ++i) v[i] = cg * fmaf(Ttot, JA[i], -JB[i]);
+      if constexpr (NEED_GRAD) ray_moments(v, gx, gy, vals);
     }
   }
   block_reduce_store<NT>(vals, red, partials + ((size_t)b * nblk + blockIdx.x) * kNAcc);
@@ -555,6 +598,7 @@ __global__ void __launch_bounds__(NT) iou_kernel(const P* __restrict__ p_true,
 using namespace sqr;
 
 // ============================================================================ C ABI
+// rays per block (the per-sample partial count depends on it only)
 static int implicit_threads(int R) { return R > 128 ? 128 : 256; }
 
 static size_t implicit_lds_bytes(int R, int NT, bool /*grad*/) {
@@ -589,12 +633,15 @@ extern "C" int sqr_implicit_loss_fwd_bwd_mean(const float* params, const float* 
   const int nblk = (R * R + NT - 1) / NT;
   float* partials = (float*)workspace;
   const dim3 grid(nblk, B);
-  const size_t lds = implicit_lds_bytes(R, NT, need_grad != 0);
   // (the gradient moments are computed whether or not they are wanted: the kernel without them
   // compiles the shared forward chain differently and its loss would differ in the last bits;
   // ImplicitLoss's value must not depend on torch.no_grad)
   // (the depth loop unrolled by 2: two voxels' independent work interleaved; B = 64 call at R = 32
   // 28.2 -> 25.7 us, config 5's R = 64 / B = 16 call 39.9 -> 37.3 us; unrolled by 4: the same)
+  // (one lane per ray: rays split over 2 / 4 lanes, their segments combined in closed form, measured
+  // the same at R = 32 / B = 64 (24.5 / 25.7 us against 24.6 per call) and slower at R = 64 / B = 64
+  // (85.3 / 104.5 against 83.5 us): profiles/r05b_loss_split_times.jsonl)
+  const size_t lds = implicit_lds_bytes(R, NT, true);
   if (NT == 256)
     hipLaunchKernelGGL((implicit_loss_kernel<256, true, 2>), grid, dim3(256), lds, st, params, target, H, W, R, tau,
                        sharpness, partials);

@@ -27,7 +27,7 @@ PROBE_KEY = ["fwd", 64, 64, 3, 1]
 # false, false, 64, 2>", the type and STATS eaten; the two flags ACC = BNB = false before the tile
 # geometry single it out among this step's instances: forward, dgrad + addend, dgrad + BatchNorm
 # operands)
-FWD_RE = re.compile(r"conv3p_kernel(IDF16b?Lb1ELb0ELb0ELi\d+ELi\d+ELb0E|<[^<>]*?,\s*true,\s*false,\s*false,\s*\d+,\s*\d+(,\s*false)?>|<bool _Accum, bool, E, false, false(, \d+, \d+(, false)?)?>)")
+FWD_RE = re.compile(r"conv3p_kernel(IDF16[b_]?Lb1ELb0ELb0ELi\d+ELi\d+ELb0E|<[^<>]*?,\s*true,\s*false,\s*false,\s*\d+,\s*\d+(,\s*false)?>|<bool _Accum, bool, E, false, false(, \d+, \d+(, false)?)?>)")
 
 
 def per_dispatch(root, counter, kernel):
