@@ -26,6 +26,25 @@
 namespace sqr {
 namespace conv {
 
+// SQR_STAMPS builds (tools/conv_stamps.py, never the shipped library): a kernel whose clock probe is
+// armed keeps five wall-clock stamps per workgroup (start, prologue done, first chunk done, main loop
+// done, stores drained) and writes them to tp[2 + 8 * blockIdx.x ...] at its end, beside blockIdx.x
+#ifdef SQR_STAMPS
+#define SQR_STAMP_DECL unsigned long long stamp_[5] = {0, 0, 0, 0, 0};
+#define SQR_STAMP(i) (stamp_[i] = wall_clock64())
+#define SQR_STAMP_WRITE(tp)                                                              \
+  do {                                                                                   \
+    if ((tp) && threadIdx.x == 0) {                                                      \
+      for (int i_ = 0; i_ < 5; ++i_) (tp)[2 + 8 * blockIdx.x + i_] = stamp_[i_];          \
+      (tp)[2 + 8 * blockIdx.x + 5] = blockIdx.x;                                         \
+    }                                                                                    \
+  } while (0)
+#else
+#define SQR_STAMP_DECL
+#define SQR_STAMP(i) ((void)0)
+#define SQR_STAMP_WRITE(tp) ((void)0)
+#endif
+
 // 16-B slot XOR key of a 128-B LDS row (see the header): shift-invariant conflict-free b128 reads
 __device__ __forceinline__ int d3key(int row) { return row & 6; }
 
@@ -199,6 +218,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
   char* const bring = smem + NWB * WIN;
   clock_begin(a.tp);
+  SQR_STAMP_DECL
+  SQR_STAMP(0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -331,6 +352,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
   }
   __builtin_amdgcn_s_barrier();
+  SQR_STAMP(1);
 
   // window fragment offsets of tap t (r, c3) for this lane's TM pixel rows
   auto tap_qoff = [&](int t, int* qo) {
@@ -457,7 +479,9 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #undef SQR_D3_STEP_WAIT
       __builtin_amdgcn_s_barrier();
     }
+    if (cc == 0) SQR_STAMP(2);
   }
+  SQR_STAMP(3);
   if constexpr (PD != 2) {  // drain the dummy loads before the epilogue reuses the LDS
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -542,6 +566,11 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
                                                  a.stats + ((size_t)tile_m * 2 + 1) * a.Nout + n0,
                                                  tile_n == 0 ? a.stats + (size_t)a.ntm * 2 * a.Nout + tile_m : nullptr,
                                                  (float)BM);
+#ifdef SQR_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  SQR_STAMP(4);
+  SQR_STAMP_WRITE(a.tp);
   clock_end(a.tp);
 }
 
@@ -1340,6 +1369,8 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   clock_begin(a.tp);
+  SQR_STAMP_DECL
+  SQR_STAMP(0);
   const int split = bid / a.ntiles, tile = bid - split * a.ntiles;
   const int k0 = (tile / a.ntc) * 64, c0 = (tile % a.ntc) * 64;
   const int ch0 = split * a.cps;
@@ -1533,6 +1564,8 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
       }
     wait_vm_chunks<PER>(min(STAGES - 2, nloc - 1));
     __builtin_amdgcn_s_barrier();
+    SQR_STAMP(1);
+    SQR_STAMP(2);  // (no chunk-0 stamp in this kernel: its chunks run as one unrolled stream)
     static_for<0, D>([&](auto jc) __attribute__((always_inline)) { issue(std::integral_constant<int, 0>{}, jc); });
     // groups of STAGES chunks with a successor, then the 1..STAGES remaining ones (the last of them
     // LAST) — straight-line bodies only: a branch between bodies inside the loop made the compiler
@@ -1560,6 +1593,7 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
   constexpr int RW = 64 * 9 + 4;  // staged row stride (floats)
   constexpr int KG = STAGES * STAGE >= 64 * RW * 4 ? 4 : 2;
   static_assert(STAGES * STAGE >= 16 * KG * RW * 4, "epilogue staging fits the pipeline's LDS");
+  SQR_STAMP(3);
   __syncthreads();  // every wave is past its last fragment read of the pipeline stages
   float* __restrict__ stg = (float*)smem;
   float* __restrict__ slab = a.slab + ((size_t)split * a.K + k0) * a.C * 9 + (size_t)c0 * 9;
@@ -1586,6 +1620,11 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
       *(f32x4*)(slab + (size_t)(16 * g + r) * krow + 4 * q) = *(const f32x4*)(stg + r * RW + 4 * q);
     }
   });
+#ifdef SQR_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  SQR_STAMP(4);
+  SQR_STAMP_WRITE(a.tp);
   clock_end(a.tp);
 }
 

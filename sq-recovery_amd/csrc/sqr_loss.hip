@@ -132,6 +132,44 @@ __device__ __forceinline__ void vox_fwd(const SQ& s, float dx, float dy, float d
   f.G = fexp2(s.e1 * f.lF);
 }
 
+// The per-ray form of vox_fwd for the ImplicitLoss walk: along a ray only gz varies, so
+// u_i = ((M_i0 dx + M_i1 dy) + M_i2 (gz - t2)) / a_i = al_i + be_i gz (RayU, formed once per ray: three
+// FMAs per voxel instead of twelve operations), and log2 A1 = 2 log2|u0| (no square, no FLT_MIN clamp:
+// a |u0| below 1e-19 keeps its true logarithm where u0^2 would underflow; the exact-zero fix of
+// classes.py:261-263 is kept).  lA..lC come out already divided by e2 / e1; the Jacobian needs
+// 1/u_i (vox_jac11), not 2^-log2 A1.
+struct RayU {
+  float al[3], be[3];
+  float lfixA, lfixB, lfixC;  // log2(1e-4) / e2, / e2, / e1 (the zero-fixed squares)
+  float i2e2, i2e1;           // 2 / e2, 2 / e1
+};
+__device__ __forceinline__ void ray_u(const SQ& s, float dx, float dy, RayU& r) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float c = fmaf(s.M[3 * i], dx, fmaf(s.M[3 * i + 1], dy, -s.M[3 * i + 2] * s.t[2]));
+    r.al[i] = c * s.ia[i];
+    r.be[i] = s.M[3 * i + 2] * s.ia[i];
+  }
+  const float l4 = flog2(1e-4f);
+  r.lfixA = l4 * s.ie2;
+  r.lfixB = l4 * s.ie2;
+  r.lfixC = l4 * s.ie1;
+  r.i2e2 = 2.f * s.ie2;
+  r.i2e1 = 2.f * s.ie1;
+}
+__device__ __forceinline__ void vox_fwd_ray(const SQ& s, const RayU& r, float gz, Vox& f) {
+  f.u0 = fmaf(r.be[0], gz, r.al[0]);
+  f.u1 = fmaf(r.be[1], gz, r.al[1]);
+  f.u2 = fmaf(r.be[2], gz, r.al[2]);
+  f.lA = f.u0 != 0.f ? flog2(fabsf(f.u0)) * r.i2e2 : r.lfixA;
+  f.lB = f.u1 != 0.f ? flog2(fabsf(f.u1)) * r.i2e2 : r.lfixB;
+  f.lC = f.u2 != 0.f ? flog2(fabsf(f.u2)) * r.i2e1 : r.lfixC;
+  f.lF1 = lse2(f.lA, f.lB, &f.rA, &f.rB);
+  f.lE = s.r21 * f.lF1;
+  f.lF = lse2(f.lE, f.lC, &f.rE, &f.rC);
+  f.G = fexp2(s.e1 * f.lF);
+}
+
 // sigmoid(sharp (1-G)) and 1-sigmoid without cancellation
 __device__ __forceinline__ void occupancy(float G, float sharp, float& occ, float& omo) {
   const float ex = fexp2(-sharp * (1.f - G) * kLog2e);
@@ -208,23 +246,25 @@ __device__ __forceinline__ void block_reduce_store(float* vals, float* red, floa
 // dL/docc = 1 at one voxel: the 11 moments of its Jacobian that vary along a ray, J[0..10] =
 // (m0..m7, m10, m13, m16): gx and gy are constant along a ray, so m8 = gx m5, m9 = gy m5,
 // m11 = gx m6, m12 = gy m6, m14 = gx m7, m15 = gy m7 are formed once per ray (ray_moments)
-__device__ __forceinline__ void vox_jac11(const SQ& s, const Vox& f, float occ, float omo, float sharp, float gz,
-                                          float* J) {
-  const float hG = -sharp * occ * omo * f.G;  // dL/dln G at dL/docc = 1
+__device__ __forceinline__ void vox_jac11(const SQ& s, const RayU& ru, const Vox& f, float occ, float omo, float nsharp,
+                                          float gz, float* J) {
+  const float hG = nsharp * occ * omo * f.G;  // dL/dln G at dL/docc = 1
   const float g_lnF = hG * s.e1;
   const float g_lnE = g_lnF * f.rE;
   const float g_lnC = g_lnF * f.rC;
   const float g_lnF1 = g_lnE * s.r21;
   const float g_lnA = g_lnF1 * f.rA, g_lnB = g_lnF1 * f.rB;
-  J[3] = kLn2 * (hG * f.lF - (g_lnE * f.lE + g_lnC * f.lC) * s.ie1);
-  J[4] = kLn2 * s.ie2 * (g_lnE * f.lE - g_lnA * f.lA - g_lnB * f.lB);
-  // d lnA1/du0 = 2 u0 / A1: the share times 2^-log2(A1) (A1 itself may sit below FLT_MIN)
-  const float gu0 = 2.f * f.u0 * s.ie2 * g_lnA * fexp2(-f.lA1);
-  const float gu1 = 2.f * f.u1 * s.ie2 * g_lnB * fexp2(-f.lB1);
-  const float gu2 = 2.f * f.u2 * s.ie1 * g_lnC * fexp2(-f.lC1);
-  J[0] = gu0 * f.u0;
-  J[1] = gu1 * f.u1;
-  J[2] = gu2 * f.u2;
+  const float eE = g_lnE * f.lE;
+  J[3] = kLn2 * (hG * f.lF - (eE + g_lnC * f.lC) * s.ie1);
+  J[4] = kLn2 * s.ie2 * (eE - g_lnA * f.lA - g_lnB * f.lB);
+  // d lnA1/du0 = 2 u0 / A1 = 2 / u0 (A1 = u0^2; an exact zero was fixed to a constant: no gradient)
+  const float c0 = ru.i2e2 * g_lnA, c1 = ru.i2e2 * g_lnB, c2 = ru.i2e1 * g_lnC;
+  const float gu0 = f.u0 != 0.f ? c0 * frcp(f.u0) : 0.f;
+  const float gu1 = f.u1 != 0.f ? c1 * frcp(f.u1) : 0.f;
+  const float gu2 = f.u2 != 0.f ? c2 * frcp(f.u2) : 0.f;
+  J[0] = f.u0 != 0.f ? c0 : 0.f;  // gu0 * u0
+  J[1] = f.u1 != 0.f ? c1 : 0.f;
+  J[2] = f.u2 != 0.f ? c2 : 0.f;
   J[5] = gu0;
   J[6] = gu1;
   J[7] = gu2;
@@ -294,28 +334,39 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
   const int ix = c, iy = R - 1 - r;  // D[r,c] = depth[x=c, y=R-1-r] (classes.py:279)
   const float gx = axis[ix], gy = axis[iy];
   const float dx = gx - s.t[0], dy = gy - s.t[1];
-  const float ntau = -tau * kLog2e;
+  const float ntau = -tau * kLog2e, nsharp = -sharp, nsl = -sharp * kLog2e;
+  RayU ru;
+  ray_u(s, dx, dy, ru);
   float S = 0.f, P = 0.f;  // occupancy sum, prefix of T
-  float JA[NM], JB[NM];    // sum J, sum P_{m-1} J_m
+  // sum J, sum P_{m-1} J_m as pairs: gfx950's packed FP32 (v_pk_add_f32 / v_pk_fma_f32) updates two
+  // moments per instruction (the last pair's second lane is padding)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int NP = (NM + 1) / 2;
+  f2 JA[NP], JB[NP];
 #pragma unroll
-  for (int i = 0; i < NM; ++i) JA[i] = JB[i] = 0.f;
+  for (int i = 0; i < NP; ++i) JA[i] = JB[i] = f2{0.f, 0.f};
   if (active) {
 #pragma unroll UNR
     for (int k = 0; k < R; ++k) {
       const float gz = axis[R - 1 - k];
       Vox f;
-      vox_fwd(s, dx, dy, gz - s.t[2], f);
-      float occ, omo;
-      occupancy(f.G, sharp, occ, omo);
+      vox_fwd_ray(s, ru, gz, f);
+      // sigmoid(sharp (1-G)) and 1 - sigmoid without cancellation (occupancy())
+      const float ex = fexp2(fmaf(-nsl, f.G, nsl));
+      const float occ = frcp(1.f + ex);
+      const float omo = (ex < 1e30f) ? ex * occ : 1.f;
       S += occ;
       const float T = fexp2(ntau * S);
       if (NEED_GRAD) {
-        float J[11];
-        vox_jac11(s, f, occ, omo, sharp, gz, J);
+        float J[12];
+        vox_jac11(s, ru, f, occ, omo, nsharp, gz, J);
+        J[11] = 0.f;
+        const f2 P2 = {P, P};
 #pragma unroll
-        for (int i = 0; i < NM; ++i) {
-          JA[i] += J[i];
-          JB[i] = fmaf(P, J[i], JB[i]);
+        for (int i = 0; i < NP; ++i) {
+          const f2 Ji = {J[2 * i], J[2 * i + 1]};
+          JA[i] += Ji;
+          JB[i] = __builtin_elementwise_fma(P2, Ji, JB[i]);
         }
       }
       P += T;
@@ -329,9 +380,12 @@ __global__ void __launch_bounds__(NT) implicit_loss_kernel(
     if (NEED_GRAD && diff != 0.f) {
       // dL/docc_m = sign(D-true) * tau/R * (Ttot - P_{m-1})   (scaled by 1/(B R^2) in finalize)
       const float cg = (diff > 0.f ? 1.f : -1.f) * tau / (float)R;
-      float v[NM];
+      float v[2 * NP];
 #pragma unroll
-      for (int i = 0; i < NM; ++i) v[i] = cg * fmaf(Ttot, JA[i], -JB[i]);
+      for (int i = 0; i < NP; ++i) {
+        v[2 * i] = cg * fmaf(Ttot, JA[i][0], -JB[i][0]);
+        v[2 * i + 1] = cg * fmaf(Ttot, JA[i][1], -JB[i][1]);
+      }
       if constexpr (NEED_GRAD) ray_moments(v, gx, gy, vals);
     }
   }
