@@ -238,9 +238,10 @@ def time_probe(tr, reps=10):
     return (float(np.mean(times)) if times else float("nan")), len(times), "kernel wall clock, eager steps"
 
 
-def time_loss_call(crit, images, B, dev, reps=20):
-    """GPU time of one fused ImplicitLoss call (forward + analytic gradient) at the bench shapes:
-    captured once in a HIP graph and replayed, so host launch gaps do not count."""
+def time_loss_call(crit, images, B, dev, reps=20, per_graph=10):
+    """GPU time of one fused ImplicitLoss call (forward + analytic gradient) at the bench shapes, as
+    it runs inside the step graph: per_graph back-to-back calls captured in one HIP graph, replayed
+    reps times, so neither host launch gaps nor the graph launch itself count."""
     pred = (torch.rand(B, 12, device=dev) * 0.5 + 0.25).requires_grad_(True)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -249,7 +250,8 @@ def time_loss_call(crit, images, B, dev, reps=20):
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        crit(images, pred)
+        for _ in range(per_graph):
+            crit(images, pred)
     g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -258,7 +260,7 @@ def time_loss_call(crit, images, B, dev, reps=20):
         g.replay()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    return e0.elapsed_time(e1) / (reps * per_graph)
 
 
 # the probe kernel's forward instance in rocprofv3 kernel names (tools/traffic.py FWD_RE: the
@@ -634,7 +636,8 @@ def run(args, json_fd):
         loss_ms = time_loss_call(tr.crit, tr.images, B, dev) if rank == 0 else None
         if loss_ms:
             tps = B * R ** 3 * LOSS_TRANSC_PER_VOXEL / (loss_ms * 1e-3) / 1e12
-            extra["implicit_loss"] = {"call_ms_graph": loss_ms, "achieved": tps, "peak": PEAK_TRANSC_TPS,
+            extra["implicit_loss"] = {"call_ms_graph": loss_ms, "timing": "10 calls per graph replay",
+                                      "achieved": tps, "peak": PEAK_TRANSC_TPS,
                                       "unit": "T transcendentals/s", "frac": tps / PEAK_TRANSC_TPS,
                                       "hbm_bytes_per_image": R * R * 4 + 96}
         out["roofline_extra"] = extra

@@ -70,22 +70,71 @@ static inline int ilog2_ceil(int x) {
 }
 
 // ---------------------------------------------------------------- wave64 reductions
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+// sums over the 64 lanes, the same value in every lane: DPP row sums (no LDS round trips, unlike a
+// __shfl_xor butterfly's six ds_bpermute levels) and the four rows' lane-15 totals through SGPRs, added
+// in a fixed order (deterministic).  Call in wave-uniform control flow (inactive lanes count as 0).
+__device__ __forceinline__ float wave_sum(float v);
+__device__ __forceinline__ double wave_sum_d(double v);
 
 __device__ __forceinline__ long long wave_sum_ll(long long v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// 16-lane ("DPP row") reductions without an LDS round trip: __shfl / __shfl_xor compile to
+// ds_bpermute_b32, whose latency a chain of them pays at every level (the statistics epilogues'
+// 9-deep chains per channel group: ~4 us of the layer-2 forward's epilogue, tools/conv_stamps.py).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, true));
+}
+// sum over the 16 lanes of each row (row_shr 1, 2, 4, 8 prefix sums): complete in the row's lane 15
+__device__ __forceinline__ float row_sum15(float x) {
+  x += dpp_f<0x111>(x);
+  x += dpp_f<0x112>(x);
+  x += dpp_f<0x114>(x);
+  x += dpp_f<0x118>(x);
+  return x;
+}
+// the value v of the first lane of this lane's row (lane & 48), broadcast to the row
+__device__ __forceinline__ float row_first(float v) {
+  const int bits = __builtin_bit_cast(int, v);
+  const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 0));
+  const float k1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 16));
+  const float k2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 32));
+  const float k3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 48));
+  const int row = (int)(threadIdx.x >> 4) & 3;
+  return row == 0 ? k0 : (row == 1 ? k1 : (row == 2 ? k2 : k3));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row_sum15(v);
+  const int b = __builtin_bit_cast(int, v);
+  return ((__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 15)) +
+           __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 31))) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 47))) +
+         __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 63));
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  const long long b = __builtin_bit_cast(long long, x);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane), hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_d<0x111>(v);
+  v += dpp_d<0x112>(v);
+  v += dpp_d<0x114>(v);
+  v += dpp_d<0x118>(v);
+  return ((readlane_d(v, 15) + readlane_d(v, 31)) + readlane_d(v, 47)) + readlane_d(v, 63);
 }
 
 // ---------------------------------------------------------------- BatchNorm statistics (Welford rows)

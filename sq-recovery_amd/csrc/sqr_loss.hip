@@ -463,7 +463,22 @@ __global__ void loss_finalize_kernel(const float* __restrict__ params, const flo
   if (b < B) {
     double acc[kNAcc];
     for (int i = 0; i < kNAcc; ++i) acc[i] = 0.0;
-    for (int k = 0; k < nblk; ++k) {
+    // the loads of 4 partials in flight at a time (a rolled loop waits for each partial's 18 loads
+    // before issuing the next ones); the summation order is unchanged
+    int k = 0;
+    for (; k + 4 <= nblk; k += 4) {
+      float v[4][kNAcc];
+      const float* src = partials + ((size_t)b * nblk + k) * kNAcc;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < kNAcc; ++i) v[u][i] = src[u * kNAcc + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < kNAcc; ++i) acc[i] += (double)v[u][i];
+    }
+    for (; k < nblk; ++k) {
       const float* src = partials + ((size_t)b * nblk + k) * kNAcc;
       for (int i = 0; i < kNAcc; ++i) acc[i] += (double)src[i];
     }

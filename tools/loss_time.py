@@ -23,7 +23,7 @@ def main():
         p = torch.tensor(classes.sample_sq_params(np.random.default_rng(0), B), device=dev)
         img = losses.implicit_render(p, H, 1.5, 260).unsqueeze(1).contiguous()
         crit = classes.ImplicitLoss(R, dev, 1.5, 260)
-        ms = bench.time_loss_call(crit, img, B, dev, reps=50)
+        ms = bench.time_loss_call(crit, img, B, dev, reps=10)
         tps = B * R ** 3 * bench.LOSS_TRANSC_PER_VOXEL / (ms * 1e-3) / 1e12
         out["R%d_H%d_B%d" % (R, H, B)] = {"us": round(ms * 1e3, 2), "frac": round(tps / bench.PEAK_TRANSC_TPS, 4)}
     print(json.dumps(out))
