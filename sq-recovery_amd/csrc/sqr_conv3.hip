@@ -1617,7 +1617,9 @@ __global__ void __launch_bounds__(256) conv3_wgrad_kernel(D3WArgs a) {
     __syncthreads();
     for (int i = tid; i < 16 * KG * 144; i += 256) {
       const int r = i / 144, q = i - r * 144;
-      *(f32x4*)(slab + (size_t)(16 * g + r) * krow + 4 * q) = *(const f32x4*)(stg + r * RW + 4 * q);
+      // nontemporal: the slab is read once, by the sum launch (same-box A/B +0.15 %,
+      // profiles/r05r_ab_wgrad_nontemporal_slab.txt)
+      __builtin_nontemporal_store(*(const f32x4*)(stg + r * RW + 4 * q), (f32x4*)(slab + (size_t)(16 * g + r) * krow + 4 * q));
     }
   });
 #ifdef SQR_STAMPS
