@@ -105,8 +105,12 @@ __global__ void fwd_finalize_kernel(const P* __restrict__ part, int nblk, int M,
   if (c >= C) return;
   // the channel's parameters are loaded first: their round trip overlaps the partials' (this
   // launch is latency-bound: a chain of dependent memory round trips)
-  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  const float rm0 = rmean ? rmean[c] : 0.f, rv0 = rmean ? rvar[c] : 0.f;
+  // (unconditional loads from a valid address, the null cases selected afterwards: a conditional load
+  // is waited for inside its branch — four serial round trips before the partials' loads)
+  const float gv = (gamma ? gamma : save_mean)[c], btv = (beta ? beta : save_mean)[c];
+  const float rmv = (rmean ? rmean : save_mean)[c], rvv = (rmean ? rvar : save_mean)[c];
+  const float g = gamma ? gv : 1.f, bt = beta ? btv : 0.f;
+  const float rm0 = rmean ? rmv : 0.f, rv0 = rmean ? rvv : 0.f;
   double mean, m2;
   merge_stats_w<P>(part, nblk, C, c, (double)M, &mean, &m2);
   if (threadIdx.x & 63) return;
@@ -131,7 +135,8 @@ __global__ void infer_coef_kernel(int C, const float* __restrict__ gamma, const 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double invstd = 1.0 / sqrt((double)rvar[c] + (double)eps);
-  const double g = gamma ? gamma[c] : 1.0, bt = beta ? beta[c] : 0.0;
+  const float gv = (gamma ? gamma : rvar)[c], btv = (beta ? beta : rvar)[c];  // (unconditional: see above)
+  const double g = gamma ? (double)gv : 1.0, bt = beta ? (double)btv : 0.0;
   coef[c] = (float)(g * invstd);
   coef[C + c] = (float)(bt - rmean[c] * g * invstd);
 }
@@ -282,8 +287,10 @@ struct FinPar {
   float g, bt, rm, rv;
 };
 __device__ __forceinline__ FinPar fin_par(const FinJob& j, int c) {
-  return FinPar{j.gamma ? j.gamma[c] : 1.f, j.beta ? j.beta[c] : 0.f, j.rmean ? j.rmean[c] : 0.f,
-                j.rmean ? j.rvar[c] : 0.f};
+  // unconditional loads from a valid address (see fwd_finalize_kernel)
+  const float gv = (j.gamma ? j.gamma : j.save_mean)[c], btv = (j.beta ? j.beta : j.save_mean)[c];
+  const float rmv = (j.rmean ? j.rmean : j.save_mean)[c], rvv = (j.rmean ? j.rvar : j.save_mean)[c];
+  return FinPar{j.gamma ? gv : 1.f, j.beta ? btv : 0.f, j.rmean ? rmv : 0.f, j.rmean ? rvv : 0.f};
 }
 __device__ __forceinline__ void fwd_finalize_one(const FinJob& j, const FinPar& p, int c, int M, int C, double mean,
                                                  double m2) {
@@ -364,13 +371,19 @@ __global__ void bwd_finalize2_kernel(const double* __restrict__ part, int nblk, 
   const bool second = w >= C;
   const FinJob& j = second ? b : a;
   const int c = second ? w - C : w;
-  const double is = j.save_invstd[c], mu = j.save_mean[c], gm = j.gamma ? j.gamma[c] : 1.0;  // before the partials
+  // before the partials, unconditionally (see fwd_finalize_kernel); the pointers picked field by
+  // field (a whole-struct pick reads the kernel arguments through memory and waits for them)
+  const float* sinv = second ? b.save_invstd : a.save_invstd;
+  const float* smean = second ? b.save_mean : a.save_mean;
+  const float* gam = second ? b.gamma : a.gamma;
+  const float isf = sinv[c], muf = smean[c], gv = (gam ? gam : sinv)[c];
   double acc[2];
   if (second)
     sum_partials_w<double, 3, 2>(part, nblk, C, c, acc);
   else
     sum_partials_w<double, 3, 1>(part, nblk, C, c, acc);
   if (threadIdx.x & 63) return;
+  const double is = isf, mu = muf, gm = gam ? (double)gv : 1.0;
   const double sg = acc[0], sgx = acc[1];
   const double dgam = sgx * is;
   if (j.dgamma) j.dgamma[c] = (float)dgam;

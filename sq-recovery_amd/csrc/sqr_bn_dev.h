@@ -229,10 +229,29 @@ template <typename P, int NS = 2, int SB = 1>
 __device__ __forceinline__ void sum_partials_w(const P* __restrict__ part, int nblk, int C, int c, double* s) {
   const int l = threadIdx.x & 63;
   double a = 0.0, b = 0.0;
+  constexpr int RMAX = 8;  // up to 512 rows: every load of the lane in one round trip
+  if (nblk <= 64 * RMAX) {
+    // branch-free (rows past nblk re-read row 0 and are dropped below); the lane's rows are summed
+    // in the same order as the loop below
+    P va[RMAX], vb[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int k = l + 64 * r, kk = k < nblk ? k : 0;
+      va[r] = part[(size_t)kk * NS * C + c];
+      vb[r] = part[(size_t)kk * NS * C + SB * C + c];
+    }
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const bool in = l + 64 * r < nblk;
+      a = in ? a + (double)va[r] : a;
+      b = in ? b + (double)vb[r] : b;
+    }
+  } else {
 #pragma unroll 4
-  for (int k = l; k < nblk; k += 64) {
-    a += (double)part[(size_t)k * NS * C + c];
-    b += (double)part[(size_t)k * NS * C + SB * C + c];
+    for (int k = l; k < nblk; k += 64) {
+      a += (double)part[(size_t)k * NS * C + c];
+      b += (double)part[(size_t)k * NS * C + SB * C + c];
+    }
   }
   s[0] = wave_sum_d(a);
   s[1] = wave_sum_d(b);
@@ -295,10 +314,13 @@ __device__ __forceinline__ void bn_bwd_finalize_w(const P* __restrict__ part, in
                                                   const float* __restrict__ gamma, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dgamma,
                                                   float* __restrict__ dbeta, float* __restrict__ coef) {
-  const double is = invstd[c], mu = mean[c], gm = gamma ? gamma[c] : 1.0;  // before the partials: overlapped
+  // the channel's parameters are loaded before the partials, unconditionally (a conditional load
+  // is converted inside its branch, which waits for it there: one more dependent round trip)
+  const float isf = invstd[c], muf = mean[c], gv = (gamma ? gamma : invstd)[c];
   double acc[2];
   sum_partials_w<P>(part, nblk, C, c, acc);
   if ((threadIdx.x & 63) != 0) return;
+  const double is = isf, mu = muf, gm = gamma ? (double)gv : 1.0;
   const double sg = acc[0], sgx = acc[1];
   const double dgam = sgx * is;  // sum g * xhat
   if (dgamma) dgamma[c] = (float)dgam;
