@@ -151,18 +151,19 @@ __global__ void __launch_bounds__(256) apply_kernel(const T* __restrict__ x, con
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nvec) return;
     const int v = i & ((1 << lv) - 1);
-    float xv[8], sc[8], sh[8];
+    // every load issued before the first use (the residual's unconditionally, from x when there is
+    // none: a load inside `if (res)` went out only after the others had landed)
+    float xv[8], sc[8], sh[8], rv[8];
     V8<T>::load(x + i * 8, xv);
     load8f(coef + v * 8, sc);
     load8f(coef + C + v * 8, sh);
+    V8<T>::load((res ? res : x) + i * 8, rv);
+    const bool hr = res != nullptr;
     float o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = fmaf(xv[k], sc[k], sh[k]);
-    if (res) {
-      float rv[8];
-      V8<T>::load(res + i * 8, rv);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+    for (int k = 0; k < 8; ++k) {
+      o[k] = fmaf(xv[k], sc[k], sh[k]);
+      o[k] = hr ? o[k] + rv[k] : o[k];  // (a select, not a branch: the load stays ahead)
     }
     if (relu) {
 #pragma unroll
@@ -200,17 +201,18 @@ __global__ void __launch_bounds__(256) bwd_apply_kernel(const T* __restrict__ dy
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nvec) return;
     const int v = i & ((1 << lv) - 1);
+    // every load issued before the first use: the mask byte unconditionally (from dy when there is
+    // none; a load inside `if (mask)` cost two extra round trips: dy's, then the mask's, before x)
     float g[8], xv[8], k1[8], k2[8], k3[8];
     V8<T>::load(dy + i * 8, g);
-    if (mask) {
-      const uint32_t mb = mask[i];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1 ? g[k] : 0.f;
-    }
+    const uint32_t mraw = (mask ? mask : (const uint8_t*)dy)[i];
     V8<T>::load(x + i * 8, xv);
     load8f(coef + v * 8, k1);
     load8f(coef + C + v * 8, k2);
     load8f(coef + 2 * C + v * 8, k3);
+    const uint32_t mb = mask ? mraw : 0xffu;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1 ? g[k] : 0.f;
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = fmaf(k1[k], g[k], fmaf(k3[k], xv[k], k2[k]));
@@ -407,11 +409,7 @@ __global__ void __launch_bounds__(256) bwd_apply2_kernel(const T* __restrict__ d
   const int v = i & ((1 << lv) - 1);
   float g[8], a[8], b[8], k[6][8];
   V8<T>::load(dy + i * 8, g);
-  if (mask) {
-    const uint32_t mb = mask[i];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = (mb >> e) & 1 ? g[e] : 0.f;
-  }
+  const uint32_t mraw = (mask ? mask : (const uint8_t*)dy)[i];  // unconditional: see bwd_apply_kernel
   V8<T>::load(xa + i * 8, a);
   V8<T>::load(xb + i * 8, b);
 #pragma unroll
@@ -419,6 +417,9 @@ __global__ void __launch_bounds__(256) bwd_apply2_kernel(const T* __restrict__ d
     load8f(ca + q * C + v * 8, k[q]);
     load8f(cb + q * C + v * 8, k[3 + q]);
   }
+  const uint32_t mb = mask ? mraw : 0xffu;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = (mb >> e) & 1 ? g[e] : 0.f;
   float oa[8], ob[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {

@@ -15,6 +15,7 @@
 // corrections: m = lerp(m, g, 1 - b1); v = b2 v + (1 - b2) g^2;
 // p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps),  t = step + 1.
 #include <stdint.h>
+#include <type_traits>
 #include "sqr_common.h"
 
 namespace sqr {
@@ -64,16 +65,29 @@ __device__ __forceinline__ void adam_update(float& p, float& m, float& v, float 
 __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   extern __shared__ float lds[];
   const int b = blockIdx.x;
-  if (J.found_inf && *J.found_inf) return;  // non-finite scaled gradient somewhere: skip the step
   int ji = 0;
   while (ji + 1 < J.njobs && b >= J.start[ji + 1]) ++ji;
   const Job& jb = J.j[ji];
   const int local = b - J.start[ji];
-  // GradScaler's unscale: g * (1 / scale) with the reciprocal rounded to fp32 as torch does
-  const float gsc = J.loss_scale ? J.gscale * (float)(1.0 / (double)*J.loss_scale) : J.gscale;
-  const double t = (double)(*jb.step) + 1.0;
-  const double bc1 = 1.0 - pow(J.b1, t), bc2 = 1.0 - pow(J.b2, t);
-  const float step_size = (float)(J.lr / bc1), bc2s = (float)sqrt(bc2);
+  // The float4 paths issue the thread's parameter / moment / gradient loads FIRST; the skip flag,
+  // the loss scale, the step counter and the float64 bias corrections (two pow) follow while those
+  // loads are in flight (computed before them, they held every workgroup's loads back by a scalar
+  // round trip and ~70 float64 instructions).
+  // the step's scalars are loaded first, unconditionally (null pointers read the step counter instead
+  // and are selected away): used only after the parameter loads have gone out
+  const int fiv = *(J.found_inf ? J.found_inf : (const int*)jb.step);
+  const float lsv = *(J.loss_scale ? J.loss_scale : jb.step);
+  const float stepv = *jb.step;
+  float gsc = 1.f, step_size = 0.f, bc2s = 1.f;
+  auto coefs = [&]() {
+    // GradScaler's unscale: g * (1 / scale) with the reciprocal rounded to fp32 as torch does
+    gsc = J.loss_scale ? J.gscale * (float)(1.0 / (double)lsv) : J.gscale;
+    const double t = (double)stepv + 1.0;
+    const double bc1 = 1.0 - pow(J.b1, t), bc2 = 1.0 - pow(J.b2, t);
+    step_size = (float)(J.lr / bc1);
+    bc2s = (float)sqrt(bc2);
+  };
+  auto skipped = [&]() { return J.found_inf && fiv; };  // non-finite scaled gradient: skip the step
   // Adam is HBM-bound (28 B per element): the float4 path keeps 16 loads of 16 B in flight per
   // thread (2 groups x p, m, v, g), the scalar path (unaligned slots, odd sizes) 4 of 4 B
   auto upd4 = [&](size_t i4, float* keep) {  // elements 4*i4 .. +3
@@ -100,18 +114,61 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
     jb.v[i] = v;
     return p;
   };
+  // RU float4 groups of the thread (group u: float4 index q[u], present when ok[u]) loaded together,
+  // then the coefficients, then updated and stored (keep: the updated values also go to LDS, group u
+  // at keep + 1024 u); false = the step is skipped
+  auto groups = [&](auto RUc, const int* q, const bool* ok, float* keep) {
+    constexpr int RU = decltype(RUc)::value;
+    f32x4 P[RU], M[RU], V[RU], G[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      if (ok[u]) {
+        P[u] = ((const f32x4*)jb.p)[q[u]];
+        M[u] = ((const f32x4*)jb.m)[q[u]];
+        V[u] = ((const f32x4*)jb.v)[q[u]];
+        G[u] = ((const f32x4*)jb.g)[q[u]];
+      }
+    }
+    if (skipped()) return false;
+    coefs();
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      if (ok[u]) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float pe = P[u][e], me = M[u][e], ve = V[u][e];
+          adam_update(pe, me, ve, gsc == 1.f ? G[u][e] : G[u][e] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s,
+                      J.eps);
+          P[u][e] = pe;
+          M[u][e] = me;
+          V[u][e] = ve;
+        }
+        ((f32x4*)jb.p)[q[u]] = P[u];
+        ((f32x4*)jb.m)[q[u]] = M[u];
+        ((f32x4*)jb.v)[q[u]] = V[u];
+        if (keep) *(f32x4*)(keep + 1024 * u) = P[u];
+      }
+    }
+    return true;
+  };
   if (!jb.krsc) {
     const int i0 = local * CHUNK;
     const int i1 = min(i0 + CHUNK, jb.n);
     if (jb.vec) {  // CHUNK = 256 threads x 2 float4; the job's tail (n % 4) in scalar
       const int q1 = i1 >> 2;
+      constexpr int RU = CHUNK / 1024;
+      int q[RU];
+      bool ok[RU];
 #pragma unroll
-      for (int u = 0; u < CHUNK / 1024; ++u) {
-        const int q = (i0 >> 2) + u * 256 + (int)threadIdx.x;
-        if (q < q1) upd4(q, nullptr);
+      for (int u = 0; u < RU; ++u) {
+        q[u] = (i0 >> 2) + u * 256 + (int)threadIdx.x;
+        ok[u] = q[u] < q1;
       }
+      if (!groups(std::integral_constant<int, RU>{}, q, ok, nullptr)) return;
       if (i1 == jb.n && (int)threadIdx.x < (jb.n & 3)) upd1((size_t)(jb.n & ~3) + threadIdx.x);
     } else {
+      if (skipped()) return;
+      coefs();
       for (int i = i0 + (int)threadIdx.x; i < i1; i += 256) upd1(i);
     }
     return;
@@ -122,46 +179,27 @@ __global__ void __launch_bounds__(256) adam_kernel(Jobs J) {
   if (jb.vec && CRS <= 4 * 256 * ROWU) {
     // the whole row in one round trip: every load of the thread is issued before the first update
     // (upd4's loads and stores alias as far as the compiler knows, so a loop of upd4 calls would
-    // serialise a memory round trip per float4 group)
-    const int n4 = CRS >> 2;
-    const size_t b4 = base >> 2;
-    f32x4 P[ROWU], M[ROWU], V[ROWU], G[ROWU];
+    // serialise a memory round trip per float4 group); the row also goes to LDS for the packing
+    const int n4 = CRS >> 2, b4 = (int)(base >> 2);
+    int q[ROWU];
+    bool ok[ROWU];
 #pragma unroll
     for (int u = 0; u < ROWU; ++u) {
-      const int q = threadIdx.x + 256 * u;
-      if (q < n4) {
-        P[u] = ((const f32x4*)jb.p)[b4 + q];
-        M[u] = ((const f32x4*)jb.m)[b4 + q];
-        V[u] = ((const f32x4*)jb.v)[b4 + q];
-        G[u] = ((const f32x4*)jb.g)[b4 + q];
-      }
+      ok[u] = (int)threadIdx.x + 256 * u < n4;
+      q[u] = b4 + (int)threadIdx.x + 256 * u;
     }
-#pragma unroll
-    for (int u = 0; u < ROWU; ++u) {
-      const int q = threadIdx.x + 256 * u;
-      if (q < n4) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float pe = P[u][e], me = M[u][e], ve = V[u][e];
-          adam_update(pe, me, ve, gsc == 1.f ? G[u][e] : G[u][e] * gsc, J.omb1, J.fb2, J.omb2, step_size, bc2s,
-                      J.eps);
-          P[u][e] = pe;
-          M[u][e] = me;
-          V[u][e] = ve;
-        }
-        ((f32x4*)jb.p)[b4 + q] = P[u];
-        ((f32x4*)jb.m)[b4 + q] = M[u];
-        ((f32x4*)jb.v)[b4 + q] = V[u];
-        *(f32x4*)(lds + 4 * q) = P[u];
-      }
-    }
+    if (!groups(std::integral_constant<int, ROWU>{}, q, ok, lds + 4 * threadIdx.x)) return;
   } else if (jb.vec) {
+    if (skipped()) return;
+    coefs();
     const int n4 = CRS >> 2;
     for (int q = threadIdx.x; q < n4; q += 512) {
       upd4((base >> 2) + q, lds + 4 * q);
       if (q + 256 < n4) upd4((base >> 2) + q + 256, lds + 4 * (q + 256));
     }
   } else {
+    if (skipped()) return;
+    coefs();
     for (int i = threadIdx.x; i < CRS; i += 256) lds[i] = upd1(base + i);
   }
   __syncthreads();
@@ -218,7 +256,18 @@ struct CJobs {
 __global__ void __launch_bounds__(256) crsk_kernel(CJobs J) {
   __shared__ uint16_t tile[64][66];
   const int b = blockIdx.x;
-  if (b == 0 && threadIdx.x < J.nsteps && !(J.found_inf && *J.found_inf)) *J.steps[threadIdx.x] += 1.f;
+  // the step counters: a workgroup of their own (the last), so that their round trips run beside the
+  // tiles' instead of in front of workgroup 0's (the launch ends with its slowest workgroup); the
+  // skip flag and the counters are loaded together
+  if (b == (int)gridDim.x - 1) {
+    if ((int)threadIdx.x < J.nsteps) {
+      const int fi = J.found_inf ? *J.found_inf : 0;
+      float* p = J.steps[threadIdx.x];
+      const float v = *p;
+      if (!fi) *p = v + 1.f;
+    }
+    return;
+  }
   if (J.njobs == 0) return;
   int ji = 0;
   while (ji + 1 < J.njobs && b >= J.start[ji + 1]) ++ji;
@@ -375,8 +424,8 @@ extern "C" int sqr_adam_step_amp(const sqr_adam_param* params, int nparams, doub
     SQR_HIP_LAUNCH_CHECK("adam_kernel");
   }
   cj.start[cj.njobs] = cblocks;
-  const int cb = cblocks > 1 ? cblocks : 1;
-  hipLaunchKernelGGL(crsk_kernel, dim3(cb), dim3(256), 0, st, cj);
+  // + 1: the step-counter workgroup
+  hipLaunchKernelGGL(crsk_kernel, dim3(cblocks + 1), dim3(256), 0, st, cj);
   SQR_HIP_LAUNCH_CHECK("crsk_kernel");
   return 0;
 }
