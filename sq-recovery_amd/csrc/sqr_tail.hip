@@ -186,9 +186,33 @@ __device__ __forceinline__ void pool_sample(const Dev& d, int n, float* feat, fl
 __device__ __forceinline__ void heads_sample(const Dev& d, int n, const float* h1, float* z, float* sv, float* out_a,
                                              float* out_e, float* out_t, float* out_q) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = wave; i < NOUT; i += 4) {
-    const int hd = head_of(i), r = head_row(i);
-    const float s = wave_dot(d.wh[hd] + (size_t)r * d.F2, h1, d.F2, lane) + d.bh[hd][r];
+  // wave w: rows w, w+4, w+8, their weight loads in flight together (one round trip, not three)
+  constexpr int RPW = NOUT / 4;
+  float acc[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) acc[q] = 0.f;
+  for (int c = lane * 4; c < d.F2; c += 256) {
+    f32x4 a[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int i = wave + 4 * q;
+      const int hd = head_of(i);  // (selects, not a kernel-argument array index: see up_grad)
+      const float* wr = hd == 0 ? d.wh[0] : hd == 1 ? d.wh[1] : hd == 2 ? d.wh[2] : d.wh[3];
+      a[q] = *(const f32x4*)(wr + (size_t)head_row(i) * d.F2 + c);
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      acc[q] = fmaf(a[q][0], h1[c], acc[q]);
+      acc[q] = fmaf(a[q][1], h1[c + 1], acc[q]);
+      acc[q] = fmaf(a[q][2], h1[c + 2], acc[q]);
+      acc[q] = fmaf(a[q][3], h1[c + 3], acc[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int i = wave + 4 * q, hd = head_of(i), r = head_row(i);
+    const float* bh = hd == 0 ? d.bh[0] : hd == 1 ? d.bh[1] : hd == 2 ? d.bh[2] : d.bh[3];
+    const float s = wave_sum(acc[q]) + bh[r];
     if (lane == 0) {
       z[i] = s;
       sv[d.C0 + d.F1 + d.F2 + i] = s;
@@ -268,11 +292,17 @@ struct Up {  // upstream gradients of a, e, t, q (nullable = zero) and their row
   int ld[4];
 };
 
-// grad of one output element (0 if that output received no gradient)
-__device__ __forceinline__ float up_grad(const Up& u, int n, int i) {
+// grad of one output element (0 if that output received no gradient); the load is unconditional
+// (`dummy`: any valid address, read when the head has no gradient) so that it goes out with the
+// others instead of being waited for inside a branch
+__device__ __forceinline__ float up_grad(const Up& u, int n, int i, const float* dummy) {
   const int hd = head_of(i), r = head_row(i);
-  const float* g = u.g[hd];
-  return g ? g[(size_t)n * u.ld[hd] + r] : 0.f;
+  // the head's pointer and stride picked by selects (an index into the kernel-argument arrays with a
+  // per-lane value is a memory load, and a wait, of its own)
+  const float* g = hd == 0 ? u.g[0] : hd == 1 ? u.g[1] : hd == 2 ? u.g[2] : u.g[3];
+  const int ld = hd == 0 ? u.ld[0] : hd == 1 ? u.ld[1] : hd == 2 ? u.ld[2] : u.ld[3];
+  const float v = *(g ? g + (size_t)n * ld + r : dummy);
+  return g ? v : 0.f;
 }
 
 // out[j] = sum_k in[k] * W[k][j] for j < ncols, k < nrows: lanes own 4 columns each (float4 rows
@@ -308,17 +338,24 @@ __global__ void __launch_bounds__(256) tail_bwd_kernel(Dev d, const float* __res
   float* ds = dsave + (size_t)n * ldd;  // [d0 F1][d1 F2][dz 12]
 
   if (tid < NOUT) {
-    const float gi = up_grad(up, n, tid), zi = zs[tid];
+    // every load first: this thread's gradient and logit, the quaternion head's four of each
+    const float gi = up_grad(up, n, tid, zs), zi = zs[tid];
+    float gq[4], zq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      gq[k] = up_grad(up, n, 8 + k, zs);
+      zq[k] = zs[8 + k];
+    }
     float r;
     if (tid < 8) {
       const float s = sigmoidf(zi);
       r = gi * (1.f - s) * s;
     } else {
       // q = z / |z|:  dz = (g - q (q . g)) / |z|
-      const float nrm = sqrtf(zs[8] * zs[8] + zs[9] * zs[9] + zs[10] * zs[10] + zs[11] * zs[11]);
+      const float nrm = sqrtf(zq[0] * zq[0] + zq[1] * zq[1] + zq[2] * zq[2] + zq[3] * zq[3]);
       float dot = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) dot = fmaf(up_grad(up, n, 8 + k), zs[8 + k] / nrm, dot);
+      for (int k = 0; k < 4; ++k) dot = fmaf(gq[k], zq[k] / nrm, dot);
       r = (gi - (zi / nrm) * dot) / nrm;
     }
     dz[tid] = r;
