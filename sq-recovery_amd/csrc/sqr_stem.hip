@@ -603,11 +603,22 @@ __global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ p
   const int c0 = blockIdx.x * 32 + 4 * q;
   double a[4] = {0.0, 0.0, 0.0, 0.0};
   if (c0 < cols) {
-#pragma unroll 8
-    for (int r = z; r < rows; r += 32) {
-      const f32x4 v = *(const f32x4*)(part + (size_t)r * cols + c0);
+    // 16 rows per lane at a time, every load of the batch issued before the first add (branch-free:
+    // rows past the end re-read row z and are dropped); rows summed in the same order as one loop
+    constexpr int RB = 16;
+    for (int rb = z; rb < rows; rb += 32 * RB) {
+      f32x4 v[RB];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) a[e] += (double)v[e];
+      for (int u = 0; u < RB; ++u) {
+        const int r = rb + 32 * u;
+        v[u] = *(const f32x4*)(part + (size_t)(r < rows ? r : z) * cols + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const bool in = rb + 32 * u < rows;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = in ? a[e] + (double)v[u][e] : a[e];
+      }
     }
   }
 #pragma unroll
@@ -634,16 +645,24 @@ __global__ void __launch_bounds__(64) stem_bwd_finalize_kernel(const double* __r
   const int k = blockIdx.x, j = threadIdx.x;
   const int r = j >> 3, s = j & 7;
   const bool real = r < 7 && s < 7;
-  wk[j] = real ? (double)(float)(T)w[k * 49 + r * 7 + s] : 0.0;
-  __syncthreads();
+  // every load first (a chain of dependent round trips otherwise): the weight (clamped index, zero
+  // on the padding taps), the sums, the column of S, the BatchNorm's saved statistics
+  const float wv = w[k * 49 + (real ? r * 7 + s : 0)];
   const double t1 = tot[k * KC + j], t3 = tot[2 * KC * KC + j];
-  double t2 = 0.0;
-  for (int i = 0; i < KC; ++i) t2 += wk[i] * tot[KC * KC + i * KC + j];
   const double sg = tot[2 * KC * KC + KC + k];
+  const float isf = invstd[k], muf = mean[k], gmf = (gamma ? gamma : invstd)[k];
+  double scol[KC];
+#pragma unroll
+  for (int i = 0; i < KC; ++i) scol[i] = tot[KC * KC + i * KC + j];
+  wk[j] = real ? (double)(float)(T)wv : 0.0;
+  __syncthreads();
+  double t2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < KC; ++i) t2 += wk[i] * scol[i];
   const double sgx = wave_sum_d(wk[j] * t1);
-  const double is = invstd[k], mu = mean[k];
+  const double is = isf, mu = muf;
   const double dgam = (sgx - mu * sg) * is;  // sum g * xhat
-  const double a = (gamma ? (double)gamma[k] : 1.0) * is;
+  const double a = (gamma ? (double)gmf : 1.0) * is;
   const double k3 = -a * is * dgam / M;
   const double k2 = -a * sg / M - k3 * mu;
   if (real) dw[k * 49 + r * 7 + s] = (float)(a * t1 + k3 * t2 + k2 * t3);
