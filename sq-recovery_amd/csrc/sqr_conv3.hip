@@ -132,7 +132,6 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
                                            int tid, float* stats_row0, float* stats_row1, float* count, float bm) {
   constexpr int WN = BN / WAVES_N;
   constexpr float NG = 16.f * TM, INV_NG = 1.f / (16.f * TM);
-  const int lane = tid & 63, lead = lane & 48;
   float* r1 = red + wm * BN + wn * WN + 4 * fq;
   float* r2 = r1 + WAVES_M * BN;
 #pragma unroll
@@ -143,7 +142,7 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
       float v[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) v[i] = (e & 1) ? hi2f<T>(pk[j][i][e >> 1]) : lo2f<T>(pk[j][i][e >> 1]);
-      const float K = __shfl(v[0], lead, 64);
+      const float K = row_first(v[0]);  // lane fr = 0 of the 16-lane row (readlane, no LDS)
       float sa = 0.f, sq = 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -151,16 +150,15 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
         sa += d;
         sq = fmaf(d, d, sq);
       }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) {
-        sa += __shfl_xor(sa, off, 64);
-        sq += __shfl_xor(sq, off, 64);
-      }
+      // DPP row sums (four row_shr adds each, totals in lane fr = 15) instead of four ds_bpermute
+      // levels per value: the epilogue's 8 * TN * 4 dependent LDS round trips were most of its time
+      sa = row_sum15(sa);
+      sq = row_sum15(sq);
       const float sn = sa * INV_NG;
       m[e] = K + sn;
       q[e] = fmaxf(sq - sa * sn, 0.f);
     }
-    if (fr == 0) {
+    if (fr == 15) {
       *(f32x4*)(r1 + 16 * j) = f32x4{m[0], m[1], m[2], m[3]};
       *(f32x4*)(r2 + 16 * j) = f32x4{q[0], q[1], q[2], q[3]};
     }
