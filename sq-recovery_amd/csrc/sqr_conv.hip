@@ -341,10 +341,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
       vf[i] = m0 + wm * WM + 16 * i + fr < g.M ? 1.f : 0.f;
       nl += vf[i];
     }
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) nl += __shfl_xor(nl, off, 64);  // the group's count
+    // DPP row sums (totals in the row's lane fr = 15, which writes) and a readlane broadcast of the
+    // row's first value: no ds_bpermute round trips (see the tiled conv's tile_stats)
+    nl = row_sum15(nl);  // the group's count
     const float inv_n = nl > 0.f ? 1.f / nl : 0.f;
-    const int lead = lane & 48;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       float cm[4], cq[4];
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
         float v[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) v[i] = (float)(T)acc[j][i][e];
-        const float K = __shfl(v[0], lead, 64);
+        const float K = row_first(v[0]);
         float sa = 0.f, sq = 0.f;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -361,16 +361,13 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
           sa += d;
           sq = fmaf(d, d, sq);
         }
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          sa += __shfl_xor(sa, off, 64);
-          sq += __shfl_xor(sq, off, 64);
-        }
+        sa = row_sum15(sa);
+        sq = row_sum15(sq);
         const float sn = sa * inv_n;
         cm[e] = K + sn;
         cq[e] = fmaxf(sq - sa * sn, 0.f);
       }
-      if (fr == 0) {
+      if (fr == 15) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int col = wn * WN + 16 * j + 4 * fq + e;

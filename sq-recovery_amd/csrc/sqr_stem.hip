@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
           const uint32_t xb = pk16<T>(acc[jb][2 * h], acc[jb][2 * h + 1]);  // the T conv output
           const f32x2 v = {plo<T>(xb), phi<T>(xb)};
           const int i = 2 * jb + h;
-          if (b == 0 && mytiles == 0) K2[i] = f32x2{__shfl(v[0], lane & 48, 64), __shfl(v[1], lane & 48, 64)};
+          if (b == 0 && mytiles == 0) K2[i] = f32x2{row_first(v[0]), row_first(v[1])};
           const f32x2 d = v - K2[i];
           S2[i] += d;
           Q2[i] = __builtin_elementwise_fma(d, d, Q2[i]);
@@ -246,18 +246,14 @@ __global__ void __launch_bounds__(256) stem_stats_kernel(const TI* __restrict__ 
   float m[16], q[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    float sa = S2[i >> 1][i & 1], sq = Q2[i >> 1][i & 1];
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) {
-      sa += __shfl_xor(sa, off, 64);
-      sq += __shfl_xor(sq, off, 64);
-    }
+    // DPP row sums: totals in the row's lane fr = 15 (which writes below)
+    const float sa = row_sum15(S2[i >> 1][i & 1]), sq = row_sum15(Q2[i >> 1][i & 1]);
     const float sn = n > 0.f ? sa / n : 0.f;
     m[i] = K2[i >> 1][i & 1] + sn;
     q[i] = fmaxf(sq - sa * sn, 0.f);
   }
   __syncthreads();
-  if (fr == 0) {
+  if (fr == 15) {
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb)
 #pragma unroll
