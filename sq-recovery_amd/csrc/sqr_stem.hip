@@ -112,9 +112,15 @@ __device__ __forceinline__ void load_wfrag(const float* __restrict__ w, int lane
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int r = 4 * ks + fq;
+      // every load unconditional (clamped index, the padding taps selected to 0 afterwards): a load
+      // under the lane-dependent `r < 7` was issued and waited for inside its branch — dozens of
+      // serial round trips in every workgroup's prologue
+      const int rc = r < 7 ? r : 6;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        wf[jb][ks][i] = (T)((r < 7 && i < 7) ? w[(16 * jb + fr) * 49 + r * 7 + i] : 0.f);
+      for (int i = 0; i < 8; ++i) {
+        const float v = w[(16 * jb + fr) * 49 + rc * 7 + (i < 7 ? i : 6)];
+        wf[jb][ks][i] = (T)((r < 7 && i < 7) ? v : 0.f);
+      }
     }
 }
 
