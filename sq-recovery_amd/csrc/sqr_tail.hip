@@ -338,14 +338,22 @@ __global__ void __launch_bounds__(256) tail_bwd_kernel(Dev d, const float* __res
   float* ds = dsave + (size_t)n * ldd;  // [d0 F1][d1 F2][dz 12]
 
   if (tid < NOUT) {
-    // every load first: this thread's gradient and logit, the quaternion head's four of each
-    const float gi = up_grad(up, n, tid, zs), zi = zs[tid];
-    float gq[4], zq[4];
+    // every load first, from uniform addresses: all 12 upstream gradients (output i's head is a
+    // compile-time constant in the unrolled loop: the head pointers stay scalar kernel arguments; a
+    // per-lane head index put them in scratch and serialised three loads) and the quaternion logits;
+    // then this thread's pair is picked by selects
+    float gall[NOUT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      gq[k] = up_grad(up, n, 8 + k, zs);
-      zq[k] = zs[8 + k];
-    }
+    for (int i = 0; i < NOUT; ++i) gall[i] = up_grad(up, n, i, zs);
+    const float zi = zs[tid];
+    float zq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) zq[k] = zs[8 + k];
+    float gi = 0.f, gq[4];
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) gi = tid == i ? gall[i] : gi;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) gq[k] = gall[8 + k];
     float r;
     if (tid < 8) {
       const float s = sigmoidf(zi);
