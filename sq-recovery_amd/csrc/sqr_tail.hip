@@ -185,21 +185,28 @@ __device__ __forceinline__ void pool_sample(const Dev& d, int n, float* feat, fl
 // the four heads of sample n from h1 (LDS): logits into sv, activated outputs
 __device__ __forceinline__ void heads_sample(const Dev& d, int n, const float* h1, float* z, float* sv, float* out_a,
                                              float* out_e, float* out_t, float* out_q) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (wave uniform in a scalar register: the head pointers below are picked by scalar selects)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // wave w: rows w, w+4, w+8, their weight loads in flight together (one round trip, not three)
   constexpr int RPW = NOUT / 4;
   float acc[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) acc[q] = 0.f;
+  // the wave's three weight rows (outputs wave, wave+4, wave+8), written out per wave so that every
+  // head pointer is a constant kernel-argument field (an index computed from the wave number made
+  // the compiler copy the pointer table to scratch and load from it)
+  const float *w0r, *w1r, *w2r;
+  switch (wave) {
+    case 0: w0r = d.wh[0]; w1r = d.wh[1] + d.F2; w2r = d.wh[3]; break;                  // a0, e1, q0
+    case 1: w0r = d.wh[0] + d.F2; w1r = d.wh[2]; w2r = d.wh[3] + d.F2; break;           // a1, t0, q1
+    case 2: w0r = d.wh[0] + 2 * d.F2; w1r = d.wh[2] + d.F2; w2r = d.wh[3] + 2 * d.F2; break;  // a2, t1, q2
+    default: w0r = d.wh[1]; w1r = d.wh[2] + 2 * d.F2; w2r = d.wh[3] + 3 * d.F2; break;  // e0, t2, q3
+  }
   for (int c = lane * 4; c < d.F2; c += 256) {
     f32x4 a[RPW];
-#pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const int i = wave + 4 * q;
-      const int hd = head_of(i);  // (selects, not a kernel-argument array index: see up_grad)
-      const float* wr = hd == 0 ? d.wh[0] : hd == 1 ? d.wh[1] : hd == 2 ? d.wh[2] : d.wh[3];
-      a[q] = *(const f32x4*)(wr + (size_t)head_row(i) * d.F2 + c);
-    }
+    a[0] = *(const f32x4*)(w0r + c);
+    a[1] = *(const f32x4*)(w1r + c);
+    a[2] = *(const f32x4*)(w2r + c);
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       acc[q] = fmaf(a[q][0], h1[c], acc[q]);
@@ -210,9 +217,23 @@ __device__ __forceinline__ void heads_sample(const Dev& d, int n, const float* h
   }
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
-    const int i = wave + 4 * q, hd = head_of(i), r = head_row(i);
-    const float* bh = hd == 0 ? d.bh[0] : hd == 1 ? d.bh[1] : hd == 2 ? d.bh[2] : d.bh[3];
-    const float s = wave_sum(acc[q]) + bh[r];
+    const int i = wave + 4 * q;
+    const float* bp;
+    switch (i) {  // (constant kernel-argument fields, as above)
+      case 0: bp = d.bh[0]; break;
+      case 1: bp = d.bh[0] + 1; break;
+      case 2: bp = d.bh[0] + 2; break;
+      case 3: bp = d.bh[1]; break;
+      case 4: bp = d.bh[1] + 1; break;
+      case 5: bp = d.bh[2]; break;
+      case 6: bp = d.bh[2] + 1; break;
+      case 7: bp = d.bh[2] + 2; break;
+      case 8: bp = d.bh[3]; break;
+      case 9: bp = d.bh[3] + 1; break;
+      case 10: bp = d.bh[3] + 2; break;
+      default: bp = d.bh[3] + 3; break;
+    }
+    const float s = wave_sum(acc[q]) + *bp;
     if (lane == 0) {
       z[i] = s;
       sv[d.C0 + d.F1 + d.F2 + i] = s;
