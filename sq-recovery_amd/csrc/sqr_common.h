@@ -72,7 +72,9 @@ static inline int ilog2_ceil(int x) {
 // ---------------------------------------------------------------- wave64 reductions
 // sums over the 64 lanes, the same value in every lane: DPP row sums (no LDS round trips, unlike a
 // __shfl_xor butterfly's six ds_bpermute levels) and the four rows' lane-15 totals through SGPRs, added
-// in a fixed order (deterministic).  Call in wave-uniform control flow (inactive lanes count as 0).
+// in a fixed order (deterministic).  All 64 lanes must be active: the row_shr DPP reads treat an
+// inactive lane as 0, but the final readlane of lanes 15/31/47/63 returns whatever an inactive lane's
+// VGPR holds (every current caller runs with the whole wave active).
 __device__ __forceinline__ float wave_sum(float v);
 __device__ __forceinline__ double wave_sum_d(double v);
 

@@ -28,13 +28,18 @@ namespace conv {
 
 // SQR_STAMPS builds (tools/conv_stamps.py, never the shipped library): a kernel whose clock probe is
 // armed keeps five wall-clock stamps per workgroup (start, prologue done, first chunk done, main loop
-// done, stores drained) and writes them to tp[2 + 8 * blockIdx.x ...] at its end, beside blockIdx.x
+// done, stores drained) and writes them to tp[2 + 8 * blockIdx.x ...] at its end, beside blockIdx.x.
+// The buffer holds SQR_STAMP_MAXWG workgroups (tools/conv_stamps.py sizes it from the same number);
+// workgroups past it keep no stamps.
 #ifdef SQR_STAMPS
+#ifndef SQR_STAMP_MAXWG
+#define SQR_STAMP_MAXWG 8192
+#endif
 #define SQR_STAMP_DECL unsigned long long stamp_[5] = {0, 0, 0, 0, 0};
 #define SQR_STAMP(i) (stamp_[i] = wall_clock64())
 #define SQR_STAMP_WRITE(tp)                                                              \
   do {                                                                                   \
-    if ((tp) && threadIdx.x == 0) {                                                      \
+    if ((tp) && threadIdx.x == 0 && blockIdx.x < SQR_STAMP_MAXWG) {                      \
       for (int i_ = 0; i_ < 5; ++i_) (tp)[2 + 8 * blockIdx.x + i_] = stamp_[i_];          \
       (tp)[2 + 8 * blockIdx.x + 5] = blockIdx.x;                                         \
     }                                                                                    \

@@ -135,9 +135,10 @@ __device__ __forceinline__ void vox_fwd(const SQ& s, float dx, float dy, float d
 // The per-ray form of vox_fwd for the ImplicitLoss walk: along a ray only gz varies, so
 // u_i = ((M_i0 dx + M_i1 dy) + M_i2 (gz - t2)) / a_i = al_i + be_i gz (RayU, formed once per ray: three
 // FMAs per voxel instead of twelve operations), and log2 A1 = 2 log2|u0| (no square, no FLT_MIN clamp:
-// a |u0| below 1e-19 keeps its true logarithm where u0^2 would underflow; the exact-zero fix of
-// classes.py:261-263 is kept).  lA..lC come out already divided by e2 / e1; the Jacobian needs
+// the zero fix of classes.py:261-263 applies exactly where the reference's fp32 square u0 * u0 is 0,
+// i.e. |u0| <= 2^-75; between that and FLT_MIN^(1/2) u0^2 is a denormal whose true logarithm is kept).  lA..lC come out already divided by e2 / e1; the Jacobian needs
 // 1/u_i (vox_jac11), not 2^-log2 A1.
+constexpr float kSqZero = 0x1p-75f;  // largest |u| whose fp32 square is 0
 struct RayU {
   float al[3], be[3];
   float lfixA, lfixB, lfixC;  // log2(1e-4) / e2, / e2, / e1 (the zero-fixed squares)
@@ -161,9 +162,11 @@ __device__ __forceinline__ void vox_fwd_ray(const SQ& s, const RayU& r, float gz
   f.u0 = fmaf(r.be[0], gz, r.al[0]);
   f.u1 = fmaf(r.be[1], gz, r.al[1]);
   f.u2 = fmaf(r.be[2], gz, r.al[2]);
-  f.lA = f.u0 != 0.f ? flog2(fabsf(f.u0)) * r.i2e2 : r.lfixA;
-  f.lB = f.u1 != 0.f ? flog2(fabsf(f.u1)) * r.i2e2 : r.lfixB;
-  f.lC = f.u2 != 0.f ? flog2(fabsf(f.u2)) * r.i2e1 : r.lfixC;
+  // the reference's fix applies where its fp32 square is 0: u * u rounds to +0 exactly when
+  // |u| <= 2^-75 (u^2 <= 2^-150, half the smallest denormal; ties to even)
+  f.lA = fabsf(f.u0) > kSqZero ? flog2(fabsf(f.u0)) * r.i2e2 : r.lfixA;
+  f.lB = fabsf(f.u1) > kSqZero ? flog2(fabsf(f.u1)) * r.i2e2 : r.lfixB;
+  f.lC = fabsf(f.u2) > kSqZero ? flog2(fabsf(f.u2)) * r.i2e1 : r.lfixC;
   f.lF1 = lse2(f.lA, f.lB, &f.rA, &f.rB);
   f.lE = s.r21 * f.lF1;
   f.lF = lse2(f.lE, f.lC, &f.rE, &f.rC);
@@ -257,14 +260,16 @@ __device__ __forceinline__ void vox_jac11(const SQ& s, const RayU& ru, const Vox
   const float eE = g_lnE * f.lE;
   J[3] = kLn2 * (hG * f.lF - (eE + g_lnC * f.lC) * s.ie1);
   J[4] = kLn2 * s.ie2 * (eE - g_lnA * f.lA - g_lnB * f.lB);
-  // d lnA1/du0 = 2 u0 / A1 = 2 / u0 (A1 = u0^2; an exact zero was fixed to a constant: no gradient)
+  // d lnA1/du0 = 2 u0 / A1 = 2 / u0 (A1 = u0^2; where the square was fixed to 1e-4 the reference's
+  // gradient 2 u0 dL/dA1 is below 1e-18 of its scale: 0)
   const float c0 = ru.i2e2 * g_lnA, c1 = ru.i2e2 * g_lnB, c2 = ru.i2e1 * g_lnC;
-  const float gu0 = f.u0 != 0.f ? c0 * frcp(f.u0) : 0.f;
-  const float gu1 = f.u1 != 0.f ? c1 * frcp(f.u1) : 0.f;
-  const float gu2 = f.u2 != 0.f ? c2 * frcp(f.u2) : 0.f;
-  J[0] = f.u0 != 0.f ? c0 : 0.f;  // gu0 * u0
-  J[1] = f.u1 != 0.f ? c1 : 0.f;
-  J[2] = f.u2 != 0.f ? c2 : 0.f;
+  const bool n0 = fabsf(f.u0) > kSqZero, n1 = fabsf(f.u1) > kSqZero, n2 = fabsf(f.u2) > kSqZero;
+  const float gu0 = n0 ? c0 * frcp(f.u0) : 0.f;
+  const float gu1 = n1 ? c1 * frcp(f.u1) : 0.f;
+  const float gu2 = n2 ? c2 * frcp(f.u2) : 0.f;
+  J[0] = n0 ? c0 : 0.f;  // gu0 * u0
+  J[1] = n1 ? c1 : 0.f;
+  J[2] = n2 ? c2 : 0.f;
   J[5] = gu0;
   J[6] = gu1;
   J[7] = gu2;

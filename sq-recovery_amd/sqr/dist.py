@@ -42,6 +42,55 @@ class CommFailure(RuntimeError):
     asynchronous error.  The communicator has been aborted (ncclCommAbort) when this is raised."""
 
 
+def _blocking_with_deadline(fn, timeout, what):
+    """Run a blocking RCCL host call (ncclCommInitRank, ncclCommFinalize/Destroy) under a host
+    deadline.  Those calls wait for every peer and cannot be polled like device work (wait_event):
+    the call runs on a daemon thread, and when it has not returned after `timeout` seconds (a peer
+    died during start-up or teardown) this rank reports it and ends the process with status 3 -- it
+    cannot abort a communicator another thread is blocked in, and no orderly teardown can follow."""
+    import threading
+    if timeout is None:  # a single rank waits for nobody
+        return fn()
+    box = {}
+    # the HIP current device is per thread: the worker calls RCCL on the caller's device
+    dev = torch.cuda.current_device() if torch.cuda.is_initialized() else None
+
+    def body():
+        try:
+            if dev is not None:
+                torch.cuda.set_device(dev)
+            box["r"] = fn()
+        except BaseException as e:  # re-raised on the caller's thread
+            box["e"] = e
+
+    th = threading.Thread(target=body, name="sqr-rccl-" + what.replace(" ", "-"), daemon=True)
+    th.start()
+    th.join(timeout)
+    if th.is_alive():
+        print("sqr.dist: %s did not return within %.0f s (a peer rank stalled or died?); exiting" % (what, timeout),
+              file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(3)
+    if "e" in box:
+        raise box["e"]
+    return box.get("r")
+
+
+def exit_on_comm_failure(main, *args, exit_fn=None):
+    """Call main(*args); on CommFailure (the communicator has been aborted, peers may be gone) print
+    the traceback and end the process with status 3 at once: an ordinary unwind would destroy the
+    captured step graph and the process group in garbage-collection order, exactly the ordering
+    finish() exists to prevent (a hang or crash at exit instead of a clean non-zero status)."""
+    try:
+        return main(*args)
+    except CommFailure:
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        (exit_fn or os._exit)(3)
+
+
 def env():
     """(rank, world_size, local_rank) from the torchrun environment (1 process => 0, 1, 0)."""
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
@@ -80,7 +129,10 @@ class Comm:
             dist.broadcast(t, 0, group=host_group())
             uid = (ctypes.c_ubyte * 128)(*t.tolist())
         h = ctypes.c_void_p()
-        check(L.sqr_comm_init_rank(ctypes.byref(h), uid, world, rank), "sqr_comm_init_rank")
+        # ncclCommInitRank waits for every rank: a peer that died after the id exchange would block here
+        _blocking_with_deadline(lambda: check(L.sqr_comm_init_rank(ctypes.byref(h), uid, world, rank),
+                                              "sqr_comm_init_rank"),
+                                HOST_TIMEOUT_S if world > 1 else None, "ncclCommInitRank")
         self.handle, self.rank, self.world, self.version = h, rank, world, ver.value
 
     def allreduce_(self, t, stream=None):
@@ -120,10 +172,13 @@ class Comm:
             raise RuntimeError("sqr.dist.Comm self-test: all-reduce gave %r, expected %r" % (t[0].item(), want))
 
     def destroy(self):
+        """ncclCommFinalize + ncclCommDestroy, under the host deadline (a peer that dies during
+        teardown would otherwise block this rank in them forever)."""
         from ._lib import check, lib
         h, self.handle = self.handle, None
         if h is not None:
-            check(lib().sqr_comm_destroy(h), "sqr_comm_destroy")
+            _blocking_with_deadline(lambda: check(lib().sqr_comm_destroy(h), "sqr_comm_destroy"),
+                                    HOST_TIMEOUT_S if self.world > 1 else None, "ncclCommFinalize/Destroy")
 
     def abort(self):
         """ncclCommAbort: stop this rank's in-flight collectives without waiting for the peers."""

@@ -257,4 +257,5 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    # a CommFailure (aborted RCCL communicator) ends the process at once with status 3
+    dist.exit_on_comm_failure(main)

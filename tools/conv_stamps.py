@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--shape", default="64,128,32,128", help="N,C,H,K (3x3 conv, square images)")
     ap.add_argument("--phase", default="fwd", choices=("fwd", "dgrad", "wgrad"))
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
-    ap.add_argument("--maxwg", type=int, default=8192)
+    ap.add_argument("--maxwg", type=int, default=8192,
+                    help="stamp buffer capacity: must equal SQR_STAMP_MAXWG of the stamps build (tools/build_stamps.sh)")
     a = ap.parse_args()
     from sqr import conv as sc
     from sqr._lib import LIB_PATH, check, lib
