@@ -64,7 +64,7 @@ class Trainer:
     step's gradients against a float64 reference)."""
 
     def __init__(self, dev, config=2, batch=64, render=0, dtype=None, graph=True, rank=0, world=1, seed=1234,
-                 dp_rehearsal=False, dp_overlap=True):
+                 dp_rehearsal=False, dp_overlap=True, dp_proxy=None, dp_bucket_mb=None):
         import classes
         import models
         from sqr import amp, dist
@@ -102,9 +102,17 @@ class Trainer:
         # world-1 libsqr RCCL communicator
         if dp_rehearsal and world == 1:
             dist.open_comm(dev)
-        if world > 1 or dp_rehearsal:
+        self.proxy = None
+        if dp_proxy is not None and world == 1:
+            # measurement only: bucket "all-reduces" are sqr_comm_proxy launches (sqr.dist.ProxyComm)
+            n, ch, bw = dp_proxy
+            self.proxy = dist.ProxyComm(n, ch, bw, dev)
+            self.gdp = dist.GraphDataParallel(self.net, self.opt, dev, overlap=dp_overlap, comm_=self.proxy,
+                                              bucket_mb=dp_bucket_mb or dist.BUCKET_MB)
+        elif world > 1 or dp_rehearsal:
             # the same data path captured (default) or eager (--graph 0); no other fallback
-            self.gdp = dist.GraphDataParallel(self.net, self.opt, dev, overlap=dp_overlap)
+            self.gdp = dist.GraphDataParallel(self.net, self.opt, dev, overlap=dp_overlap,
+                                              bucket_mb=dp_bucket_mb or dist.BUCKET_MB)
         self.grad_seed = torch.ones((), dtype=torch.float64, device=dev)
         self.graph = None
         self.static_loss = None
@@ -471,6 +479,12 @@ def main():
     ap.add_argument("--dp-overlap", type=int, default=1, choices=(0, 1),
                     help="1: bucketed all-reduces on a side stream during the backward; 0: one all-reduce of the "
                          "whole gradient buffer after the backward, on the compute stream")
+    ap.add_argument("--dp-proxy", default="",
+                    help="N=1 measurement: NRANKS,CHANNELS,BUSBW_GBS -- each gradient bucket all-reduce becomes a "
+                         "stand-in that occupies CHANNELS workgroups for the ring time of an NRANKS-GPU all-reduce "
+                         "at BUSBW_GBS (sqr.dist.ProxyComm); with --dp-overlap 1/0 it runs beside / after the backward")
+    ap.add_argument("--dp-bucket-mb", type=float, default=0,
+                    help="gradient bucket size in MB for the overlapped all-reduce (0: sqr.dist.BUCKET_MB)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole train step in a HIP graph (1/0; default: on)")
     ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"),
@@ -523,7 +537,10 @@ def run(args, json_fd):
         dtype = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(args.dtype)
         tr = Trainer(dev, config=args.config, batch=args.batch, render=args.render, dtype=dtype,
                      graph=args.graph != 0 and cuda, rank=rank, world=world, dp_rehearsal=args.dp_rehearsal,
-                     dp_overlap=bool(args.dp_overlap))
+                     dp_overlap=bool(args.dp_overlap),
+                     dp_proxy=(tuple(float(v) for v in args.dp_proxy.split(",")) if args.dp_proxy and cuda
+                               else None),
+                     dp_bucket_mb=args.dp_bucket_mb or None)
         B, H, R = tr.B, tr.H, tr.R
         probe_clock = None
         if tr.use_graph and not args.profile:
@@ -581,6 +598,11 @@ def run(args, json_fd):
                    % ("graph-captured" if tr.graph is not None else "eager", tr.gdp.mode, c.version, c.world))
                   if tr.gdp is not None and c is not None else
                   ("eager %s over gloo" % tr.gdp.mode if tr.gdp is not None else None))}
+    if tr.proxy is not None:
+        out["dp"] = "graph-captured %s, %s (measurement stand-in at N=1: %s)" % (
+            tr.gdp.mode, tr.proxy.describe(), ", ".join("%.1f MB / %.0f us" % (b / 1e6, h)
+                                                        for b, h in tr.proxy.calls[:len(tr.gdp.buckets)]))
+        out["dp_proxy"] = True
     if not cuda:
         out["device"] = "cpu (host path over gloo: plumbing, not a throughput claim)"
     if tr.scaler is not None:

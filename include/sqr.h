@@ -500,6 +500,13 @@ int sqr_comm_async_error(sqr_comm_t comm);
 int sqr_comm_destroy(sqr_comm_t comm);
 int sqr_comm_abort(sqr_comm_t comm);
 
+/* Measurement stand-in for one bucket all-reduce at N = 1 (bench.py --dp-proxy, sqr.dist.ProxyComm;
+ * no training path calls it): `channels` 256-thread workgroups copy `bytes` from src to scratch and
+ * hold their CU until hold_us has passed since they started -- the CU slots and HBM traffic an RCCL
+ * ring all-reduce of that bucket takes on an N-GPU node, so the interference of the overlapped
+ * all-reduce with the backward kernels can be measured on a one-GPU box. */
+int sqr_comm_proxy(const void* src, void* scratch, size_t bytes, int channels, double hold_us, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

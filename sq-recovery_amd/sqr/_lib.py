@@ -186,6 +186,7 @@ SIGNATURES = {
     "sqr_comm_async_error": (c_int, [c_void_p]),
     "sqr_comm_destroy": (c_int, [c_void_p]),
     "sqr_comm_abort": (c_int, [c_void_p]),
+    "sqr_comm_proxy": (c_int, [c_void_p, c_void_p, c_size_t, c_int, ctypes.c_double, c_void_p]),
 }
 
 

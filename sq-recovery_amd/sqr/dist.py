@@ -188,6 +188,50 @@ class Comm:
             lib().sqr_comm_abort(h)
 
 
+class ProxyComm:
+    """Measurement stand-in for an N-rank RCCL communicator on ONE GPU (bench.py --dp-proxy; VERDICT
+    r05 item 4): world 1 for every semantic purpose (no broadcast, gradients unchanged, the optimizer
+    scale stays 1), but each bucket "all-reduce" launches libsqr's sqr_comm_proxy on the stream it is
+    given: `channels` resident workgroups (RCCL's channel blocks) that read the bucket, write a scratch
+    copy (the HBM side of the ring's traffic) and keep their CU until the modelled ring time,
+    2 (N - 1) / N * bytes / busbw, has passed.  Timing the captured step with it overlapped (side
+    stream, during the backward) against the same proxy after the backward (--dp-overlap 0) measures
+    what the overlap costs the backward kernels, which are sized one workgroup per CU."""
+
+    world = 1
+    version = 0
+
+    def __init__(self, nranks=8, channels=16, busbw_gbs=300.0, device="cuda"):
+        self.nranks, self.channels, self.busbw = int(nranks), int(channels), float(busbw_gbs)
+        self.device = torch.device(device)
+        self.scratch = None
+        self.calls = []  # (bytes, hold_us) per launch, in order
+
+    def hold_us(self, nbytes):
+        return 2.0 * (self.nranks - 1) / self.nranks * nbytes / (self.busbw * 1e9) * 1e6
+
+    def allreduce_(self, t, stream=None):
+        from ._lib import check, lib
+        nbytes = t.numel() * t.element_size()
+        if self.scratch is None or self.scratch.numel() * 4 < nbytes:
+            self.scratch = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=self.device)
+        hold = self.hold_us(nbytes)
+        self.calls.append((nbytes, hold))
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        check(lib().sqr_comm_proxy(ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(self.scratch.data_ptr()), nbytes,
+                                   self.channels, hold, ctypes.c_void_p(s)), "sqr_comm_proxy")
+
+    def broadcast_(self, t, root=0):
+        pass
+
+    def check(self):
+        pass
+
+    def describe(self):
+        return "proxy of a %d-rank ring all-reduce: %d channel workgroups, busbw %.0f GB/s" % (
+            self.nranks, self.channels, self.busbw)
+
+
 _comm = [None]
 
 
