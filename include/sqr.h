@@ -179,13 +179,20 @@ int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_c
                          int* stats_rows, void* workspace, size_t workspace_bytes, void* stream);
 /* sqr_conv2d_fwd_stats of x_act = relu(x_pre * scale + shift), the preceding BatchNorm + ReLU applied
  * while the conv stages its input (a BasicBlock's bn1 -> relu -> conv2, torchvision resnet18 in
- * torch/models.py:181).  coef = [scale C][shift C] (sqr_bn_fwd_finalize).  x_act and x_mask (1 bit per
- * element, as sqr_bn_fwd writes it) are written as side outputs, bitwise what sqr_bn_apply writes.
- * Persistent layer-1 shapes only (16-bit, C = K = 64, 3x3 / s1 / p1, 64- or 128-wide maps):
- * SQR_E_UNSUPPORTED otherwise, nothing launched. */
+ * torch/models.py:181).  coef = [scale C][shift C] (sqr_bn_fwd_finalize).  With x_act and x_mask (1 bit
+ * per element, as sqr_bn_fwd writes it) they are written as side outputs, bitwise what sqr_bn_apply
+ * writes: persistent layer-1 shapes only (16-bit, C = K = 64, 3x3 / s1 / p1, 64- or 128-wide maps).
+ * With both NULL nothing but y and the statistics is written (the activation never reaches memory in
+ * the forward; sqr_conv2d_bwd_data_bn_act rebuilds it in the backward): the shapes of
+ * sqr_conv2d_bnin_nso_supported.  SQR_E_UNSUPPORTED otherwise, nothing launched. */
 int sqr_conv2d_fwd_stats_bnin(const void* x_pre, const float* coef, void* x_act, uint8_t* x_mask,
                               const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats, int* stats_rows,
                               void* stream);
+/* 1 if conv d (C -> K) as the consumer of a BatchNorm + ReLU runs without the activation in memory:
+ * sqr_conv2d_fwd_stats_bnin with x_act = x_mask = NULL and sqr_conv2d_bwd_data_bn_act are both
+ * handled by direct kernels at this shape (16-bit 3x3 / s1 / p1; ResNetSQ's layer 1-4 convs at 256^2
+ * and 512^2 input and batch 64), else 0. */
+int sqr_conv2d_bnin_nso_supported(const sqr_conv_desc* d);
 /* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1
  * implicit GEMM per output-parity class (no work on structurally zero taps), all classes in one
  * launch; bf16 3x3/s2 shapes of ResNetSQ's layers 2-4 take the direct window kernel instead. */
@@ -223,6 +230,15 @@ size_t sqr_conv2d_bwd_data_bn_stats_floats(const sqr_conv_desc* d);
 int sqr_conv2d_bwd_data_bn(const void* dy, const void* w_crsk, void* g_out, const void* bn_x,
                            const uint8_t* relu_mask, const float* bn_mean, float* stats, int* stats_rows,
                            const sqr_conv_desc* d, void* workspace, size_t workspace_bytes, void* stream);
+/* sqr_conv2d_bwd_data_bn for a BatchNorm + ReLU applied on load without side outputs (the forward was
+ * sqr_conv2d_fwd_stats_bnin with x_act = x_mask = NULL): the ReLU mask is recomputed from bn_x and the
+ * forward coefficients bn_coef = [scale C][shift C] (the rounded activation > 0, as sqr_bn_apply forms
+ * it), and act_out (nullable) receives the activation relu(bn_x * scale + shift) itself -- bitwise what
+ * sqr_bn_apply writes -- for the conv's weight gradient.  Direct kernels only (the shapes of
+ * sqr_conv2d_bnin_nso_supported): SQR_E_UNSUPPORTED otherwise. */
+int sqr_conv2d_bwd_data_bn_act(const void* dy, const void* w_crsk, void* g_out, const void* bn_x,
+                               const float* bn_coef, const float* bn_mean, void* act_out, float* stats,
+                               int* stats_rows, const sqr_conv_desc* d, void* stream);
 /* x [N,H,W,C], dy [N,Ho,Wo,K] -> dw_kcrs f32 [K,C,R,S] (torch's weight-grad layout) */
 int sqr_conv2d_bwd_weight(const void* x, const void* dy, float* dw_kcrs, const sqr_conv_desc* d,
                           void* workspace, size_t workspace_bytes, void* stream);

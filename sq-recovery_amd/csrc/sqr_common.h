@@ -99,15 +99,11 @@ __device__ __forceinline__ float row_sum15(float x) {
   x += dpp_f<0x118>(x);
   return x;
 }
-// the value v of the first lane of this lane's row (lane & 48), broadcast to the row
+// the value v of the first lane of this lane's row (lane & 48), broadcast to the row: one DPP
+// row_newbcast:0 move (the four readlanes + a select it replaces serialised every statistics epilogue
+// on SGPR round trips).  Lane 0 of each row must be active.
 __device__ __forceinline__ float row_first(float v) {
-  const int bits = __builtin_bit_cast(int, v);
-  const float k0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 0));
-  const float k1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 16));
-  const float k2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 32));
-  const float k3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(bits, 48));
-  const int row = (int)(threadIdx.x >> 4) & 3;
-  return row == 0 ? k0 : (row == 1 ? k1 : (row == 2 ? k2 : k3));
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150, 0xf, 0xf, false));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -341,13 +341,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
       vf[i] = m0 + wm * WM + 16 * i + fr < g.M ? 1.f : 0.f;
       nl += vf[i];
     }
-    // DPP row sums (totals in the row's lane fr = 15, which writes) and a readlane broadcast of the
-    // row's first value: no ds_bpermute round trips (see the tiled conv's tile_stats)
+    // DPP row sums (totals in the row's lane fr = 15, which writes) and a DPP broadcast of the row's
+    // first value: no ds_bpermute round trips (see the tiled conv's tile_stats); all TN * 4 chains
+    // before one guarded write (a write per j split them into serial groups)
     nl = row_sum15(nl);  // the group's count
     const float inv_n = nl > 0.f ? 1.f / nl : 0.f;
+    float cm[TN][4], cq[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      float cm[4], cq[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float v[TM];
@@ -364,18 +365,20 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv_nt_kernel(NTMulti
         sa = row_sum15(sa);
         sq = row_sum15(sq);
         const float sn = sa * inv_n;
-        cm[e] = K + sn;
-        cq[e] = fmaxf(sq - sa * sn, 0.f);
+        cm[j][e] = K + sn;
+        cq[j][e] = fmaxf(sq - sa * sn, 0.f);
       }
-      if (fr == 15) {
+    }
+    if (fr == 15) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int col = wn * WN + 16 * j + 4 * fq + e;
           red[(wm * BN + col) * 3] = nl;
-          red[(wm * BN + col) * 3 + 1] = nl > 0.f ? cm[e] : 0.f;
-          red[(wm * BN + col) * 3 + 2] = nl > 0.f ? cq[e] : 0.f;
+          red[(wm * BN + col) * 3 + 1] = nl > 0.f ? cm[j][e] : 0.f;
+          red[(wm * BN + col) * 3 + 2] = nl > 0.f ? cq[j][e] : 0.f;
         }
-      }
     }
     __syncthreads();
     for (int t = tid; t < BN; t += NT) {
@@ -1348,8 +1351,8 @@ extern "C" int sqr_conv2d_fwd_stats_bnin(const void* x_pre, const float* coef, v
   Shape sh;
   int rc = check_desc(d, &sh);
   if (rc) return rc;
-  SQR_CHECK_ARG(x_pre && coef && x_act && x_mask && w_krsc && y && stats && stats_rows,
-                "conv2d_fwd_stats_bnin: null pointer");
+  SQR_CHECK_ARG(x_pre && coef && w_krsc && y && stats && stats_rows && (!x_act) == (!x_mask),
+                "conv2d_fwd_stats_bnin: null pointer (x_act and x_mask: both or neither)");
   if (!direct3(d, sh)) {
     set_error("conv2d_fwd_stats_bnin: only 16-bit 3x3 / stride 1 / pad 1 convs");
     return SQR_E_UNSUPPORTED;
@@ -1358,8 +1361,10 @@ extern "C" int sqr_conv2d_fwd_stats_bnin(const void* x_pre, const float* coef, v
   rc = conv3_launch(d->dtype, x_pre, w_krsc, y, d->N, d->H, d->W, d->C, d->K, 0, stats, stats_rows, as_stream(stream),
                     nullptr, nullptr, 1, nullptr, &b);
   if (rc == kNotHandled) {
-    set_error("conv2d_fwd_stats_bnin: only the persistent layer-1 kernel's shapes (64 -> 64 channels, 64- or "
-              "128-wide maps)");
+    set_error(x_act ? "conv2d_fwd_stats_bnin: side outputs only on the persistent layer-1 kernel's shapes (64 -> 64 "
+                      "channels, 64- or 128-wide maps)"
+                    : "conv2d_fwd_stats_bnin: no direct kernel with apply-on-load for this shape "
+                      "(sqr_conv2d_bnin_nso_supported)");
     return SQR_E_UNSUPPORTED;
   }
   return rc;
@@ -1545,6 +1550,36 @@ extern "C" int sqr_conv2d_bwd_data_bn(const void* dy, const void* w_crsk, void* 
   if (rc) return rc;
   return bn_mask_reduce(g_out, bn_x, relu_mask, bn_mean, (long long)d->N * d->H * d->W, d->C, d->dtype, stats,
                         stats_rows, st);
+}
+
+extern "C" int sqr_conv2d_bnin_nso_supported(const sqr_conv_desc* d) {
+  Shape sh;
+  if (!d || check_desc(d, &sh) || !direct3(d, sh)) return 0;
+  return conv3_bnin_nso_ok(d->N, d->H, d->W, d->C, d->K);
+}
+
+extern "C" int sqr_conv2d_bwd_data_bn_act(const void* dy, const void* w_crsk, void* g_out, const void* bn_x,
+                                          const float* bn_coef, const float* bn_mean, void* act_out, float* stats,
+                                          int* stats_rows, const sqr_conv_desc* d, void* stream) {
+  Shape sh;
+  int rc = check_desc(d, &sh);
+  if (rc) return rc;
+  SQR_CHECK_ARG(dy && w_crsk && g_out && bn_x && bn_coef && bn_mean && stats && stats_rows,
+                "conv2d_bwd_data_bn_act: null pointer");
+  if (!direct3(d, sh)) {
+    set_error("conv2d_bwd_data_bn_act: only 16-bit 3x3 / stride 1 / pad 1 convs");
+    return SQR_E_UNSUPPORTED;
+  }
+  BnbArgs bnb = {bn_x, nullptr, bn_mean};
+  bnb.coef = bn_coef;
+  bnb.act = act_out;
+  rc = conv3_launch(d->dtype, dy, w_crsk, g_out, d->N, d->H, d->W, d->K, d->C, 1, stats, stats_rows, as_stream(stream),
+                    nullptr, &bnb);
+  if (rc == kNotHandled) {
+    set_error("conv2d_bwd_data_bn_act: no direct kernel for this shape (sqr_conv2d_bnin_nso_supported)");
+    return SQR_E_UNSUPPORTED;
+  }
+  return rc;
 }
 
 // implicit-GEMM backward-data over the output parity classes

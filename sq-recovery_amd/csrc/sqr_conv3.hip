@@ -71,6 +71,10 @@ struct D3Args {
   const void* bn_x;        // BNB: the following BatchNorm's input [N][H][W][Nout], its ReLU mask and
   const uint8_t* bn_mask;  //      batch mean: out = conv * mask, stats = (sum g, sum g*(x - mean))
   const float* bn_mean;
+  const float* bn_coef;  // BNB, nullable: the mask is recomputed from bn_x and the BatchNorm's forward
+                         // [2][Nout] (scale, shift) instead of read from bn_mask ...
+  void* bn_act;          // ... and, if set, the activation relu(bn_x * scale + shift) is written here
+  const float* in_coef;  // BNIN: [2][Cin] (scale, shift) of the preceding BatchNorm + ReLU, applied on load
   float* stats;     // nullable: BatchNorm partials [ntm][2][Nout]
   int N, H, W, Cin, Nout;  // H, W: the OUTPUT size
   int iH, iW;              // the input size (= H, W at stride 1; 2H, 2W at stride 2)
@@ -79,7 +83,18 @@ struct D3Args {
   int flip;
   uint32_t xbytes, wbytes;
   unsigned long long* tp;  // nullable: clock probe slots
+#ifdef SQR_EXPERIMENTS
+  int exp;  // ablation bits (experiment builds only, tools/build_exp.sh): 2 no output stores, 4 no MFMAs,
+            // 8 no in-loop weight DMA (wrong results: timing only)
+#endif
 };
+
+// SQR_EXPERIMENTS builds: ablation bit test (always false in the shipped library)
+#ifdef SQR_EXPERIMENTS
+#define SQR_ABL(a, bit) (((a).exp & (bit)) != 0)
+#else
+#define SQR_ABL(a, bit) false
+#endif
 
 // one 1-KiB LDS-DMA piece (16 B per lane to dst + 16*lane)
 __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t srd, char* dst, uint32_t voff, int soff) {
@@ -139,15 +154,17 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
   constexpr float NG = 16.f * TM, INV_NG = 1.f / (16.f * TM);
   float* r1 = red + wm * BN + wn * WN + 4 * fq;
   float* r2 = r1 + WAVES_M * BN;
+  // all TN * 4 channel chains first, then one guarded write: a write per j inside the loop split the
+  // chains into TN serial groups (an exec-masked branch between them)
+  float m[TN][4], q[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    float m[4], q[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float v[TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) v[i] = (e & 1) ? hi2f<T>(pk[j][i][e >> 1]) : lo2f<T>(pk[j][i][e >> 1]);
-      const float K = row_first(v[0]);  // lane fr = 0 of the 16-lane row (readlane, no LDS)
+      const float K = row_first(v[0]);  // lane fr = 0 of the 16-lane row (DPP broadcast, no LDS)
       float sa = 0.f, sq = 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -160,12 +177,15 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
       sa = row_sum15(sa);
       sq = row_sum15(sq);
       const float sn = sa * INV_NG;
-      m[e] = K + sn;
-      q[e] = fmaxf(sq - sa * sn, 0.f);
+      m[j][e] = K + sn;
+      q[j][e] = fmaxf(sq - sa * sn, 0.f);
     }
-    if (fr == 15) {
-      *(f32x4*)(r1 + 16 * j) = f32x4{m[0], m[1], m[2], m[3]};
-      *(f32x4*)(r2 + 16 * j) = f32x4{q[0], q[1], q[2], q[3]};
+  }
+  if (fr == 15) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      *(f32x4*)(r1 + 16 * j) = f32x4{m[j][0], m[j][1], m[j][2], m[j][3]};
+      *(f32x4*)(r2 + 16 * j) = f32x4{q[j][0], q[j][1], q[j][2], q[j][3]};
     }
   }
   __syncthreads();
@@ -187,7 +207,18 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 // burst at the end (measured at B=64: +3.9 us on layer 2 when read in the epilogue).
 // BNB (backward-data into a BatchNorm+ReLU backward): x and the mask bits at the lane's outputs are
 // loaded before the main loop like ACC's addend; the stored value is g = conv * mask and the tile's
-// partial row of a.stats gets the BatchNorm backward sums (sum g, sum g*(x - mean)).
+// partial row of a.stats gets the BatchNorm backward sums (sum g, sum g*(x - mean)).  With a.bn_coef
+// the mask is not read: it is recomputed from x and the BatchNorm's forward (scale, shift) exactly as
+// the apply pass forms it (the rounded activation > 0), and the activation itself can be written
+// (a.bn_act: the weight gradient's input, never stored by the forward -- BNIN below).
+// BNIN (forward, stride 1): the input x is the PRE-activation of a BatchNorm + ReLU whose (scale,
+// shift) are a.in_coef: each chunk's halo window is transformed in LDS to relu(x * scale + shift),
+// bitwise what the apply pass writes, after it lands and before anyone reads it -- every lane rewrites
+// the 16-B pieces its own LDS-DMA fetched (padding pieces stay zero: the conv pads the activation).
+// A lane's pieces all hold the same 8 channels of a chunk (slot pslot ^ (prow & 6); hence no K20
+// window key): its 16 coefficients of a chunk are 4 LDS reads from a [2][Cin] table staged in the
+// prologue (no global load inside the loop: a compiler-tracked load there made the compiler drain
+// every in-flight weight tile before its first use).
 // S = 2 (forward of a 3x3 / stride-2 / pad-1 conv, IMGS = 1, no flip): the (2TH+1) x (2TW+1) input
 // window of a TH x TW output tile is staged as four phase planes (a, b) = (input row, column parity
 // relative to the window origin), each TW+1 pixels wide (plane (., 1) has one unused column), plane
@@ -199,7 +230,7 @@ __device__ __forceinline__ void tile_stats(const uint32_t (*pk)[TM][2], float* r
 #define SQR_D3_WINPF 1
 #endif
 template <typename T, int BM, int BN, int WAVES_M, int WAVES_N, int TW, int TH, int NWB, int IMGS = 1, int PD = 2,
-          bool ACC = false, bool BNB = false, int S = 1>
+          bool ACC = false, bool BNB = false, int S = 1, bool BNIN = false>
 __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a) {
   constexpr int NT = 64 * WAVES_M * WAVES_N, NW = WAVES_M * WAVES_N;
   constexpr int ROWB = 128, STAGES = PD + 1;
@@ -207,7 +238,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   constexpr int TM = WM / 16, TN = WN / 16;
   static_assert(S == 1 || (S == 2 && IMGS == 1 && !ACC && !BNB), "stride 2: forward, one image per tile");
   constexpr int WWID = S == 1 ? TW + 2 : TW + 1;
-  constexpr bool K20 = S == 1 && TW == 8;  // window rows keyed by k20key (8-pixel-wide tiles)
+  static_assert(!BNIN || (S == 1 && !ACC && !BNB), "apply-on-load: stride-1 forward");
+  constexpr bool K20 = S == 1 && TW == 8 && !BNIN;  // window rows keyed by k20key (8-pixel-wide tiles)
   constexpr int P0 = (TH + 1) * WWID, P1 = TH * WWID;  // stride 2: rows of an a = 0 / a = 1 plane
   constexpr int WRI = S == 1 ? (TH + 2) * WWID : 2 * P0 + 2 * P1, WR = IMGS * WRI;  // halo window rows
   constexpr int WROWS = (WR + 8 * NW - 1) / (8 * NW) * (8 * NW);
@@ -218,7 +250,10 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   constexpr int WIN = WROWS * ROWB, TILE_B = BN * ROWB;
   constexpr int LDS = NWB * WIN + STAGES * TILE_B;
   static_assert(2 * WAVES_M * 16 * BN * 4 <= LDS, "stats scratch fits the ring");
-  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+  // BNIN: the coefficient table [scale Cin][shift Cin] after the ring, in the same LDS array (a second
+  // __shared__ object made the compiler wait for every in-flight LDS-DMA before each window read)
+  __shared__ __attribute__((aligned(1024))) char smem[LDS + (BNIN ? 2 * 512 * 4 : 0)];
+  float* const ctab = (float*)(smem + LDS);
   char* const bring = smem + NWB * WIN;
   clock_begin(a.tp);
   SQR_STAMP_DECL
@@ -257,7 +292,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         av[j][i] = *(const u32x2*)(ad + o + 16 * j);
-        if constexpr (BNB) bmk[j][i] = a.bn_mask[(o + 16 * j) >> 3];
+        if constexpr (BNB) bmk[j][i] = a.bn_coef ? 0u : a.bn_mask[(o + 16 * j) >> 3];
         if constexpr (ACC) bmk[j][i] = a.addend_mask ? a.addend_mask[(o + 16 * j) >> 3] : 0xffu;
       }
     }
@@ -334,7 +369,8 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
   const int nch = a.Cin >> 6;
   const int flip = a.flip;
   const int nsteps = nch * 9;
-  static_assert(NWB == 2 || PD == 2, "single-window configurations keep the 3-stage ring");
+  // NWB = 1: one window buffer, never reloaded -- Cin = 64 (one chunk) only (pick / pick_s2f)
+  constexpr int WPN = NWB == 2 ? WP : 0;  // window pieces a deep-ring step issues at tap 0
   static_assert(PB * (PD - 1) + WP <= 63, "vmcnt range");
   static_assert(PD >= 2 && PD <= 8, "the next window must be older than the tile retired at tap 8");
   // weight tile of global step q = 9 * chunk + tap (clamped: the dummy reloads past the end keep
@@ -345,6 +381,45 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     dma_pieces<PB, NW>(wsrd, bring + ((q % STAGES) * TILE_B), bvoff,
                        __builtin_amdgcn_readfirstlane((tq * a.Cin + cq * 64) * 2), wave);
   };
+  // BNIN: this lane's 8 channels of a chunk (slot lslot) and their (scale, shift); the window pieces a
+  // lane fetched are rewritten in place once landed (bn_in_window), padding pieces left zero
+  const int lslot = pslot ^ (prow & 6);
+  // the coefficient table (2 Cin <= 4 NT floats: one 16-B load per thread, issued before the prologue's
+  // DMA and written to LDS after it, so the load's latency overlaps the DMA's)
+  static_assert(!BNIN || 2 * 512 <= 4 * NT, "coefficient table: one load per thread");
+  f32x4 ctv = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (BNIN) {
+    if (tid < a.Cin / 2) ctv = *(const f32x4*)(a.in_coef + 4 * tid);
+  }
+  f32x4 icf[BNIN ? 4 : 1];
+  auto load_icoef = [&](int ch) {
+    if constexpr (BNIN) {
+      const float* c = ctab + ch * 64 + lslot * 8;
+      icf[0] = *(const f32x4*)c;
+      icf[1] = *(const f32x4*)(c + 4);
+      icf[2] = *(const f32x4*)(c + a.Cin);
+      icf[3] = *(const f32x4*)(c + a.Cin + 4);
+    }
+  };
+  auto bn_in_window = [&](char* wbuf) {
+    if constexpr (BNIN) {
+#pragma unroll
+      for (int i = 0; i < WP; ++i) {
+        if (wvoff[i] != kOOB) {
+          u32x4* pp = (u32x4*)(wbuf + ((i * NW + wave) * 8) * ROWB + lane * 16);
+          u32x4 v = *pp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float sc0 = icf[e >> 1][2 * (e & 1)], sc1 = icf[e >> 1][2 * (e & 1) + 1];
+            const float sh0 = icf[2 + (e >> 1)][2 * (e & 1)], sh1 = icf[2 + (e >> 1)][2 * (e & 1) + 1];
+            v[e] = pack2<T>(fmaxf(fmaf(lo2f<T>(v[e]), sc0, sh0), 0.f), fmaxf(fmaf(hi2f<T>(v[e]), sc1, sh1), 0.f));
+          }
+          *pp = v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
   dma_pieces<WP, NW>(xsrd, smem, wvoff, 0, wave);
 #pragma unroll
   for (int q = 0; q < PD; ++q) issue_w(q);
@@ -353,6 +428,12 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(PB * (PD - 1)) : "memory");
+  }
+  if constexpr (BNIN) {
+    if (tid < a.Cin / 2) *(f32x4*)(ctab + 4 * tid) = ctv;
+    __syncthreads();  // the coefficient table
+    load_icoef(0);
+    bn_in_window(smem);
   }
   __builtin_amdgcn_s_barrier();
   SQR_STAMP(1);
@@ -406,7 +487,7 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
                                wave);
         } else {
           issue_w(step + PD);
-          if (t == 0)  // next chunk's window (the last chunk reloads its own into the idle buffer)
+          if (NWB == 2 && t == 0)  // next chunk's window (the last chunk reloads its own into the idle buffer)
             dma_pieces<WP, NW>(xsrd, smem + ((cc + 1) & 1) * WIN, wvoff,
                                __builtin_amdgcn_readfirstlane((next ? cc + 1 : cc) * 128), wave);
         }
@@ -429,12 +510,19 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           qf[i] = kWinPrefetch && sub == 0 && t > 0 ? qn[i] : *(const V8<T>*)(win + (qoff[i] ^ (sub << 6)));
+        if (SQR_ABL(a, 4)) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+          for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(pf[j]));
 #pragma unroll
-          for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
+          for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(qf[i]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[j][i] = mfma(pf[j], qf[i], acc[j][i]);
+        }
       }
-      issue_step();
+      if (!SQR_ABL(a, 8) || t == 0) issue_step();
       // the next tap's first window fragments, read before this step's barrier: the window of a
       // chunk is stable through its 9 taps (only the weight stage needs the barrier), so after it
       // only the weight fragments' LDS latency stands between the barrier and the first MFMA
@@ -474,12 +562,18 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
         // retire weight tile step+1 (issued at step+1-PD): younger are tiles step+2 .. step+PD and,
         // for t <= PD-1, this chunk's window load (issued at t = 0 after that step's tile load)
         if (t <= PD - 1) {
-          SQR_D3_STEP_WAIT(PB * (PD - 1) + WP);
+          SQR_D3_STEP_WAIT(PB * (PD - 1) + WPN);
         } else {
           SQR_D3_STEP_WAIT(PB * (PD - 1));
         }
       }
 #undef SQR_D3_STEP_WAIT
+      // the next chunk's window has landed (the step-end wait of tap 8 retires it): BatchNorm + ReLU
+      // applied in place before the barrier that publishes it
+      if (BNIN && t == 8 && next) {
+        load_icoef(cc + 1);
+        bn_in_window(smem + ((cc + 1) & 1) * WIN);
+      }
       __builtin_amdgcn_s_barrier();
     }
     if (cc == 0) SQR_STAMP(2);
@@ -518,20 +612,42 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
       pk[j][i][0] = pack2<T>(acc[j][i][0], acc[j][i][1]);
       pk[j][i][1] = pack2<T>(acc[j][i][2], acc[j][i][3]);
     }
+  // BNB with a.bn_coef: the lane's activation relu(x * scale + shift) (packed as the apply pass packs
+  // it) and its ReLU mask, from x and the BatchNorm's forward coefficients
+  uint32_t ak[BNB ? TN : 1][BNB ? TM : 1][2];
   if constexpr (BNB) {  // g = conv * mask (4 channels of the lane: mask bits (opix & 4) .. +3)
-    float s1[TN][4], s2[TN][4], mu[TN][4];
+    const bool bc = a.bn_coef != nullptr;
+    float s1[TN][4], s2[TN][4], mu[TN][4], csc[TN][4], csh[TN][4];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        const int c = n0 + wn * WN + 16 * j + 4 * fq + e;
         s1[j][e] = s2[j][e] = 0.f;
-        mu[j][e] = a.bn_mean[n0 + wn * WN + 16 * j + 4 * fq + e];
+        mu[j][e] = a.bn_mean[c];
+        // (loads from a selected valid pointer: no load behind the null test)
+        const float* cp = bc ? a.bn_coef : a.bn_mean;
+        csc[j][e] = cp[c];
+        csh[j][e] = cp[bc ? a.Nout + c : c];
       }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const uint32_t mb = (bmk[j][i] >> ((opix[i] + 16 * j) & 4)) & 0xfu;
+        uint32_t mb;
+        if (bc) {
+          mb = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t v = pack2<T>(fmaxf(fmaf(lo2f<T>(av[j][i][h]), csc[j][2 * h], csh[j][2 * h]), 0.f),
+                                        fmaxf(fmaf(hi2f<T>(av[j][i][h]), csc[j][2 * h + 1], csh[j][2 * h + 1]), 0.f));
+            ak[j][i][h] = v;
+            mb |= (lo2f<T>(v) > 0.f ? 1u : 0u) << (2 * h);
+            mb |= (hi2f<T>(v) > 0.f ? 1u : 0u) << (2 * h + 1);
+          }
+        } else {
+          mb = (bmk[j][i] >> ((opix[i] + 16 * j) & 4)) & 0xfu;
+        }
         pk[j][i][0] &= ((mb & 1u) ? 0xffffu : 0u) | ((mb & 2u) ? 0xffff0000u : 0u);
         pk[j][i][1] &= ((mb & 4u) ? 0xffffu : 0u) | ((mb & 8u) ? 0xffff0000u : 0u);
 #pragma unroll
@@ -561,7 +677,14 @@ __global__ void __launch_bounds__(64 * WAVES_M * WAVES_N) conv3_kernel(D3Args a)
     for (int j = 0; j < TN; j += 2) {
       const auto r0 = __builtin_amdgcn_permlane16_swap(pk[j][i][0], pk[j + 1][i][0], false, false);
       const auto r1 = __builtin_amdgcn_permlane16_swap(pk[j][i][1], pk[j + 1][i][1], false, false);
-      *(u32x4*)(out + opix[i] + 16 * j + sw) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+      if (!SQR_ABL(a, 2)) *(u32x4*)(out + opix[i] + 16 * j + sw) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+      if constexpr (BNB) {
+        if (a.bn_act) {  // the activation, same layout
+          const auto q0 = __builtin_amdgcn_permlane16_swap(ak[j][i][0], ak[j + 1][i][0], false, false);
+          const auto q1 = __builtin_amdgcn_permlane16_swap(ak[j][i][1], ak[j + 1][i][1], false, false);
+          *(u32x4*)((uint16_t*)a.bn_act + opix[i] + 16 * j + sw) = u32x4{q0[0], q1[0], q0[1], q1[1]};
+        }
+      }
     }
   if (!BNB && a.stats)
     tile_stats<T, BN, WAVES_M, WAVES_N, TM, TN, NT>(pk, (float*)smem, wm, wn, fr, fq, tid,
@@ -602,10 +725,13 @@ struct D3PArgs {
   const void* bn_x;        // BNB launches: the following BatchNorm's input x [N][H][TW][64] ...
   const uint8_t* bn_mask;  // ... its ReLU mask (1 bit / element) and ...
   const float* bn_mean;    // ... its batch mean: out = dgrad * mask, stats = its backward sums
+  const float* bn_coef;    // BNB, nullable: mask recomputed from bn_x and the forward [2][64] (scale, shift)
+  void* bn_act;            // BNB with bn_coef, nullable: the activation relu(bn_x * scale + shift) written here
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
   const float* in_coef;  // BNIN launches: x is the PRE-activation of the preceding BatchNorm + ReLU,
   void* in_act;          // [2][64] its (scale, shift): the conv reads relu(x * scale + shift) and writes
   uint8_t* in_mask;      // that activation (in_act) and its ReLU mask (1 bit / element) as side outputs
+                         // (both null: no side outputs -- the BNB dgrad of the backward rebuilds them)
   int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
   unsigned long long* tp;  // nullable: clock probe slots
@@ -736,7 +862,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
           mb |= (lo2f<T>(v[e]) > 0.f ? 1u : 0u) << (2 * e);
           mb |= (hi2f<T>(v[e]) > 0.f ? 1u : 0u) << (2 * e + 1);
         }
-        if (row >= hb && row < hb + TH * ntile) {
+        if (a.in_act && row >= hb && row < hb + TH * ntile) {
           const size_t pix = ((size_t)img * H + row) * TW + w;
           *(u32x4*)((char*)a.in_act + pix * C * 2 + cg * 16) = v;
           a.in_mask[pix * 8 + cg] = (uint8_t)mb;
@@ -761,7 +887,15 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   u32x4 av[NST];  // ACC: the addend pieces of the tile stored next; BNB: the BatchNorm input x there
   uint32_t bm[(BNB || ACC) ? NST : 1];  // BNB / masked ACC: the mask byte of each piece (8 channels)
   float bs1[BNB ? 8 : 1], bs2[BNB ? 8 : 1], bmu[BNB ? 8 : 1];  // BNB: this thread's 8 channels (tid & 7)
+  float bsc[BNB ? 8 : 1], bsh[BNB ? 8 : 1];  // BNB with bn_coef: their forward (scale, shift)
+  const bool bcoef = BNB && a.bn_coef != nullptr;
   if constexpr (BNB) {
+    const float* cp = bcoef ? a.bn_coef : a.bn_mean;  // (a valid pointer either way: no load behind a test)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bsc[e] = cp[(tid & 7) * 8 + e];
+      bsh[e] = cp[(bcoef ? 64 : 0) + (tid & 7) * 8 + e];
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       bs1[e] = bs2[e] = 0.f;
@@ -772,13 +906,18 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     const size_t tile0 = ((size_t)img * H + hb + k * TH) * TW * BN;  // first element of tile k
     const char* src = (const char*)(BNB ? a.bn_x : a.addend) + tile0 * 2;
     av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
-    if constexpr (BNB) bm[q] = a.bn_mask[tile0 / 8 + q * NT + tid];
+    if constexpr (BNB) bm[q] = bcoef ? 0u : a.bn_mask[tile0 / 8 + q * NT + tid];
     if constexpr (ACC) bm[q] = a.addend_mask ? a.addend_mask[tile0 / 8 + q * NT + tid] : 0xffu;
   };
   // (use = false: a tile that does not exist -- the stores go out of the buffer's range and are
   // dropped; issuing them anyway keeps the vector-memory instruction count the same on every path,
   // so the compiler's vmcnt waits for the row registers never include these stores)
   const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.xbytes, 0x00020000);
+  // BNB: the activation output (a store is issued for every piece either way -- out of range when
+  // there is none -- so that every path has the same vector-memory instruction count)
+  const bool bact = BNB && bcoef && a.bn_act != nullptr;
+  const __amdgpu_buffer_rsrc_t asrd =
+      __builtin_amdgcn_make_buffer_rsrc(bact ? a.bn_act : a.out, 0, a.xbytes, 0x00020000);
   auto store_piece = [&](int k, bool use, int q) {
     const uint32_t dst = use ? (uint32_t)(((img * H + hb + k * TH) * TW * BN) * 2) : kOOB;
     {
@@ -811,9 +950,22 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         }
       }
       if constexpr (BNB) {
+        uint32_t mbyte = bm[q];
+        u32x4 act = {0u, 0u, 0u, 0u};
+        if (bcoef) {  // the activation and its mask, exactly as the apply pass forms them
+          mbyte = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            act[e] = pack2<T>(fmaxf(fmaf(lo2f<T>(av[q][e]), bsc[2 * e], bsh[2 * e]), 0.f),
+                              fmaxf(fmaf(hi2f<T>(av[q][e]), bsc[2 * e + 1], bsh[2 * e + 1]), 0.f));
+            mbyte |= (lo2f<T>(act[e]) > 0.f ? 1u : 0u) << (2 * e);
+            mbyte |= (hi2f<T>(act[e]) > 0.f ? 1u : 0u) << (2 * e + 1);
+          }
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(act, asrd, (use && bact ? dst : kOOB) | (uint32_t)(c * 16), 0, 0);
 #pragma unroll
         for (int e = 0; e < 4 && use; ++e) {
-          const uint32_t keep = (((bm[q] >> (2 * e)) & 1u) ? 0xffffu : 0u) | (((bm[q] >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u);
+          const uint32_t keep = (((mbyte >> (2 * e)) & 1u) ? 0xffffu : 0u) | (((mbyte >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u);
           v[e] &= keep;  // g = dgrad * mask (masked halves become +0)
           const float g0 = lo2f<T>(v[e]), g1 = hi2f<T>(v[e]);
           bs1[2 * e] += g0;
@@ -1639,6 +1791,13 @@ struct D3Cfg {
 };
 
 int g_direct = 1;  // 0 off, 1 on when the grid is big enough, 2 whenever the shape fits
+#ifdef SQR_EXPERIMENTS
+// experiment builds: SQR_D3_CFG / SQR_S2F_CFG force a candidate id, SQR_EXP sets the ablation bits
+int env_int(const char* n, int dflt) {
+  const char* v = getenv(n);
+  return v && *v ? atoi(v) : dflt;
+}
+#endif
 int g_persist = 1;  // layer-1 persistent kernel (0: the tiled conv3_kernel; tests compare the two)
 
 
@@ -1667,8 +1826,18 @@ bool pick(int N, int H, int W, int Cin, int Nout, D3Cfg* out) {
       {3, 64, 128, 256, 8, 8, 2, 1},     // W 8 (layer4, odd batch)
       {4, 256, 64, 256, 16, 16, 2, 1},   // W 16, whole image per tile (slower than id 2 on layer3)
       {6, 256, 32, 256, 8, 8, 2, 4},     // 8 x 8, four images per tile
+#ifdef SQR_EXPERIMENTS
+      {20, 128, 64, 256, 16, 8, 2, 1},   // W 16 (layer3), 72 KiB: two workgroups per CU
+      {21, 128, 64, 256, 32, 4, 2, 1},   // W 32 (layer2), 80 KiB: two workgroups per CU
+#endif
   };
+#ifdef SQR_EXPERIMENTS
+  static const int force = env_int("SQR_D3_CFG", -1);
+#else
+  constexpr int force = -1;
+#endif
   for (const D3Cfg& c : cands) {
+    if (force >= 0 && c.id != force) continue;
     if (c.id == 0 && !(Nout == 64 && nch == 1)) continue;
     if (c.id != 0 && Nout % c.BN) continue;
     if (W % c.TW || H % c.TH) continue;
@@ -1764,8 +1933,21 @@ bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
       {0, 128, 128, 512, 32, 4, 1},  // Cin 64, Wo 32 (layer 2; 512x512: Wo 64)
       {1, 64, 128, 256, 16, 4, 2},   // Wo 16 (layer 3; 512x512: layer 3 at Wo 32)
       {2, 64, 128, 256, 8, 8, 2},    // Wo 8 (layer 4; 512x512: Wo 16)
+#ifdef SQR_EXPERIMENTS
+      {10, 128, 128, 512, 32, 4, 1},  // id 0 with a 5-stage weight ring (160 KiB)
+      {11, 64, 128, 256, 16, 4, 2},   // id 1, 5-stage ring
+      {12, 64, 128, 256, 8, 8, 2},    // id 2, 5-stage ring
+      {13, 64, 64, 256, 32, 2, 1},    // Cin 64: 2 x 32 output tiles, 68 KiB (two workgroups per CU)
+      {14, 64, 64, 256, 16, 4, 1},    // Cin 64: 4 x 16 output tiles, 64 KiB (two workgroups per CU)
+#endif
   };
+#ifdef SQR_EXPERIMENTS
+  static const int force = env_int("SQR_S2F_CFG", -1);
+#else
+  constexpr int force = -1;
+#endif
   for (const D3S2FCfg& c : cands) {
+    if (force >= 0 && c.id != force) continue;
     if ((c.nwb == 1) != (nch == 1)) continue;
     if (Nout % c.BN || Wo % c.TW || Ho % c.TH) continue;
     if ((long long)N * (Ho / c.TH) * (Wo / c.TW) * (Nout / c.BN) < 128 && g_direct < 2) continue;
@@ -1776,13 +1958,29 @@ bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
 }
 }  // namespace
 
+// tiled configurations with an apply-on-load (BNIN) instantiation
+bool bnin_tiled_id(int id) { return id == 7 || id == 8 || id == 10; }
+constexpr int kBninMaxC = 512;  // conv3_kernel's BNIN coefficient table
+
+int conv3_bnin_nso_ok(int N, int H, int W, int C, int K) {
+  if (g_direct == 0 || C % 64 || K % 64 || pow2_log(W) < 0) return 0;
+  if (C == 64 && K == 64 && (W == 64 || W == 128) && H % (W == 64 ? 2 : 1) == 0 && g_persist) return 1;
+  D3Cfg f, b;
+  // the forward (C -> K, BNIN) and the backward-data (K -> C, BNB with coefficients) both direct
+  return C <= kBninMaxC && pick(N, H, W, C, K, &f) && bnin_tiled_id(f.id) && pick(N, H, W, K, C, &b) ? 1 : 0;
+}
+
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
                  float* stats, int* stats_rows, hipStream_t st, const void* addend, const BnbArgs* bnb, int stride,
                  const uint8_t* addend_mask, const BnInArgs* bnin) {
   if (addend_mask && (!addend || stride != 1)) return kNotHandled;
-  if (bnin && (stride != 1 || flip || addend || bnb || !stats || Cin != 64 || Nout != 64 || (W != 64 && W != 128) ||
-               H % (W == 64 ? 2 : 1) || !g_persist))
-    return kNotHandled;  // apply-on-load: the persistent layer-1 forward only
+  const bool persist_shape = Cin == 64 && Nout == 64 && (W == 64 || W == 128) && H % (W == 64 ? 2 : 1) == 0 && g_persist;
+  if (bnin) {  // apply-on-load: stride-1 forwards with statistics
+    if (stride != 1 || flip || addend || bnb || !stats || (!bnin->act) != (!bnin->mask)) return kNotHandled;
+    // with side outputs (activation + mask): the persistent layer-1 kernel only
+    if (bnin->act && !persist_shape) return kNotHandled;
+  }
+  if (bnb && bnb->act && !bnb->coef) return kNotHandled;  // the activation output needs the coefficients
   if (g_direct == 0) return kNotHandled;
   if (stride == 2) {  // forward only (H, W: the input size)
     if (flip || addend || bnb || H % 2 || W % 2 || Cin % 64 || Nout % 64) return kNotHandled;
@@ -1811,12 +2009,23 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     a.wbytes = (uint32_t)wbytes;
     a.tp = probe_clock_take();
     if (stats_rows) *stats_rows = a.ntm;
+#ifdef SQR_EXPERIMENTS
+    a.exp = env_int("SQR_EXP", 0);
+    if (a.exp & 1) a.stats = nullptr;
+#endif
     const dim3 grid(a.ntm * a.ntn), blk(c.threads);
     probe_begin(st);
     SQR_DISPATCH16(dtype, T, {
       switch (c.id) {
         case 0: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 32, 4, 1, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
         case 1: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 16, 4, 2, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
+#ifdef SQR_EXPERIMENTS
+        case 10: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 32, 4, 1, 1, 4, false, false, 2>), grid, blk, 0, st, a); break;
+        case 11: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 16, 4, 2, 1, 4, false, false, 2>), grid, blk, 0, st, a); break;
+        case 12: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2, 1, 4, false, false, 2>), grid, blk, 0, st, a); break;
+        case 13: hipLaunchKernelGGL((conv3_kernel<T, 64, 64, 2, 2, 32, 2, 1, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
+        case 14: hipLaunchKernelGGL((conv3_kernel<T, 64, 64, 2, 2, 16, 4, 1, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
+#endif
         default: hipLaunchKernelGGL((conv3_kernel<T, 64, 128, 2, 2, 8, 8, 2, 1, 2, false, false, 2>), grid, blk, 0, st, a); break;
       }
     });
@@ -1853,6 +2062,8 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     p.bn_x = bnb ? bnb->x : nullptr;
     p.bn_mask = bnb ? bnb->mask : nullptr;
     p.bn_mean = bnb ? bnb->mean : nullptr;
+    p.bn_coef = bnb ? bnb->coef : nullptr;
+    p.bn_act = bnb ? bnb->act : nullptr;
     p.stats = stats;
     p.in_coef = bnin ? bnin->coef : nullptr;
     p.in_act = bnin ? bnin->act : nullptr;
@@ -1892,6 +2103,14 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   }
   D3Cfg c;
   if (!pick(N, H, W, Cin, Nout, &c)) return kNotHandled;
+  if (bnin && (!bnin_tiled_id(c.id) || Cin > kBninMaxC)) return kNotHandled;
+#ifdef SQR_EXPERIMENTS
+#define SQR_D3_EXP_CASES(ACC_, BNB_)                                                                                 \
+    case 20: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 16, 8, 2, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
+    case 21: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 32, 4, 2, 1, 2, ACC_, BNB_>), grid, blk, 0, st, a); break;
+#else
+#define SQR_D3_EXP_CASES(ACC_, BNB_)
+#endif
   D3Args a;
   a.x = x;
   a.w = w;
@@ -1901,6 +2120,9 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   a.bn_x = bnb ? bnb->x : nullptr;
   a.bn_mask = bnb ? bnb->mask : nullptr;
   a.bn_mean = bnb ? bnb->mean : nullptr;
+  a.bn_coef = bnb ? bnb->coef : nullptr;
+  a.bn_act = bnb ? bnb->act : nullptr;
+  a.in_coef = bnin ? bnin->coef : nullptr;
   a.stats = stats;
   a.N = N;
   a.H = H;
@@ -1918,6 +2140,10 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
   a.wbytes = (uint32_t)wbytes;
   a.tp = probe_clock_take();
   if (stats_rows) *stats_rows = a.ntm;
+#ifdef SQR_EXPERIMENTS
+  a.exp = env_int("SQR_EXP", 0);
+  if (a.exp & 1) a.stats = nullptr;
+#endif
   const dim3 grid(a.ntm * a.ntn), blk(c.threads);
   probe_begin(st);
 #define SQR_D3_CASES(ACC_, BNB_)                                                                                   \
@@ -1932,10 +2158,19 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 3, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
     case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5, ACC_, BNB_>), grid, blk, 0, st, a); break;   \
     case 9: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 5, ACC_, BNB_>), grid, blk, 0, st, a); break;     \
+    SQR_D3_EXP_CASES(ACC_, BNB_)                                                                                   \
     default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8, ACC_, BNB_>), grid, blk, 0, st, a); break;    \
   }
   SQR_DISPATCH16(dtype, T, {
-    if (bnb) {
+    if (bnin) {
+      // apply-on-load instantiations: the first-choice tiles of ResNetSQ's layers 2-4 at 256 / 512 input
+      switch (c.id) {
+        // (id 7's tile with the 3-stage ring: the 4-stage one fills the 160 KiB without the table)
+        case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 2, false, false, 1, true>), grid, blk, 0, st, a); break;
+        case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5, false, false, 1, true>), grid, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8, false, false, 1, true>), grid, blk, 0, st, a); break;
+      }
+    } else if (bnb) {
       SQR_D3_CASES(false, true)
     } else if (addend) {
       SQR_D3_CASES(true, false)

@@ -158,15 +158,18 @@ struct BnbArgs {
   const void* x;
   const uint8_t* mask;
   const float* mean;
+  const float* coef = nullptr;  // non-null: the mask is recomputed from x and the forward [2][C] (scale, shift)
+  void* act = nullptr;          // non-null (with coef): the activation relu(x * scale + shift) is written too
 };
 // addend (nullable, backward-data only): out = conv + addend, fused into the epilogue;
 // bnb (nullable, backward-data only): see BnbArgs (stats / stats_rows then receive its partials)
 // stride 2 (forward only, flip 0, no addend / bnb): H, W are the input size
 // addend_mask (nullable, with addend, stride 1): the addend is added only where its bit is set (a
 // ReLU-masked gradient read as (dy, mask) instead of a materialised copy)
-// the preceding BatchNorm + ReLU applied on load (forward of the persistent layer-1 kernel only, with
-// stats): x is that BatchNorm's input, coef its [2][64] (scale, shift); the activation and its ReLU
-// mask are written out as side outputs
+// the preceding BatchNorm + ReLU applied on load (stride-1 forwards with stats): x is that BatchNorm's
+// input, coef its [2][Cin] (scale, shift); act / mask (the persistent layer-1 kernel only) receive the
+// activation and its ReLU mask as side outputs, or are both null (no side outputs: the backward-data
+// launch with BnbArgs::coef rebuilds them)
 struct BnInArgs {
   const float* coef;
   void* act;
@@ -176,6 +179,10 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
                  float* stats, int* stats_rows, hipStream_t st, const void* addend = nullptr,
                  const BnbArgs* bnb = nullptr, int stride = 1, const uint8_t* addend_mask = nullptr,
                  const BnInArgs* bnin = nullptr);
+// 1 if a bn1 -> ReLU -> conv (C -> K, 3x3 / s1 / p1, 16-bit) runs entirely on direct kernels without the
+// activation in memory: the forward applies on load without side outputs and the backward-data (K -> C)
+// recomputes the mask and writes the activation (BnbArgs::coef / act)
+int conv3_bnin_nso_ok(int N, int H, int W, int C, int K);
 // direct 3x3/stride-2/pad-1 bf16 backward-data over the four output-parity classes (w_cls = the
 // packed parity-class weights of sqr_conv2d_pack_weight, cls_off in elements): kNotHandled = not handled
 // addend_s2 (with addend): the addend is compact [N][Ho][Wo][C] and lands on the (even, even) dX

@@ -97,6 +97,7 @@ SIGNATURES = {
                                      ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_fwd_stats_bnin": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                           ctypes.POINTER(SqrConvDesc), c_void_p, ctypes.POINTER(c_int), c_void_p]),
+    "sqr_conv2d_bnin_nso_supported": (c_int, [ctypes.POINTER(SqrConvDesc)]),
     "sqr_bn_fwd_finalize": (c_int, [c_void_p, c_int, ctypes.c_longlong, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_float, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "sqr_bn_apply": (c_int, [c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
@@ -113,6 +114,8 @@ SIGNATURES = {
     "sqr_conv2d_bwd_data_bn": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                        ctypes.POINTER(c_int), ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t,
                                        c_void_p]),
+    "sqr_conv2d_bwd_data_bn_act": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(SqrConvDesc), c_void_p]),
     "sqr_bn_bwd_stats": (c_int, [c_void_p, c_void_p, ctypes.c_longlong, c_int, c_int, c_void_p, c_int, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "sqr_conv2d_bwd_weight": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,

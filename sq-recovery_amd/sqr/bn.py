@@ -59,7 +59,8 @@ class BNActFn(torch.autograd.Function):
                                             ptr(bias), rm, rv, ctypes.c_float(momentum), ctypes.c_float(eps),
                                             ptr(mean), ptr(invstd), ptr(coef), stream_ptr(x.device)),
                   "sqr_bn_fwd_finalize")
-            _pending[y.data_ptr()] = (x, coef, mask)
+            ctx.deferred = Deferred(x, coef, mask, y)
+            _pending[y.data_ptr()] = ctx.deferred
         elif training and stats is not None:  # batch statistics from the producing conv's epilogue
             n = _ws_bytes(M, C)
             ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
@@ -74,6 +75,8 @@ class BNActFn(torch.autograd.Function):
                                    ctypes.c_float(momentum), ctypes.c_float(eps), int(training), ptr(residual),
                                    int(relu), ptr(y), ptr(mask), ptr(mean), ptr(invstd), ptr(ws), n,
                                    stream_ptr(x.device)), "sqr_bn_fwd")
+        if not hasattr(ctx, "deferred"):
+            ctx.deferred = None
         ctx.relu, ctx.training, ctx.eps = relu, training, eps
         ctx.has_res = residual is not None
         ctx.res_join = res_join  # sqr.conv.ResidualJoin of the residual input: its gradient is deposited
@@ -81,6 +84,7 @@ class BNActFn(torch.autograd.Function):
         ctx.link = link if (training and relu and residual is None and mask is not None) else None
         if ctx.link is not None:
             ctx.link.x, ctx.link.mask, ctx.link.mean, ctx.link.invstd = x, mask, mean, invstd
+            ctx.link.deferred = ctx.deferred
             ctx.link.gamma, ctx.link.pids = weight, (id(weight), id(bias))
         # sqr.conv.BnOutLink: the next block's conv1 reduces this BN's backward sums in its launch
         ctx.out_link = out_link if (training and relu and mask is not None) else None
@@ -97,6 +101,7 @@ class BNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, ym, weight, m, v = ctx.saved_tensors  # ym: ReLU mask (training) or y (eval)
         dy = dy.to(x.dtype).contiguous(memory_format=_CL)
+        deferred, ctx.deferred = ctx.deferred, None
         N, C, H, W = x.shape
         M = N * H * W
         if not ctx.training:  # eval-mode backward (running statistics are constants): plain torch
@@ -122,6 +127,8 @@ class BNActFn(torch.autograd.Function):
         ws = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
         part = ctx.out_link.take(dy) if ctx.out_link is not None else None
         if part is not None:  # the next block's conv1 already reduced (dy, mask, x) in its launch
+            if deferred is not None:
+                deferred.materialize()
             check(lib().sqr_bn_bwd_part(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(part[0]), part[1],
                                         ptr(weight), ptr(m), ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta),
                                         ptr(ws), n, stream_ptr(x.device)), "sqr_bn_bwd_part")
@@ -146,6 +153,8 @@ class BNActFn(torch.autograd.Function):
                                          stream_ptr(x.device)), "sqr_bn_bwd_stats")
             gradbuf.written(ctx.pids)
             return dx, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
+        if deferred is not None:  # the ReLU mask was never written (apply-on-load without side outputs)
+            deferred.materialize()
         check(lib().sqr_bn_bwd(ptr(dy), ptr(ym), ptr(x), ctypes.c_longlong(M), C, _dt(x), ptr(weight), ptr(m),
                                ptr(v), ptr(dx), ptr(dres), ptr(dgamma), ptr(dbeta), ptr(ws), n,
                                stream_ptr(x.device)), "sqr_bn_bwd")
@@ -211,8 +220,33 @@ def bn_act(x, bn, residual=None, relu=True, counted=False, res_join=None, link=N
                       _check_stats(stats, x), res_join if residual is not None else None, link, out_link, bool(defer))
     pend = _pending.pop(y.data_ptr(), None)
     if pend is not None:
-        y._sqr_bnin = pend  # (BatchNorm input, coef, ReLU mask): sqr.conv applies it on load
+        y._sqr_bnin = pend  # sqr.bn.Deferred: sqr.conv applies it on load
     return y
+
+
+class Deferred:
+    """A BatchNorm + ReLU output y = relu(x * scale + shift) whose apply pass was deferred to the
+    conv that consumes it (bn_act(defer=True); coef = [scale C][shift C]).  y and its ReLU mask start
+    unwritten.  The consuming conv either writes both as side outputs of its apply-on-load forward, or
+    -- without side outputs (sqr_conv2d_fwd_stats_bnin with NULL outputs) -- its backward-data rebuilds
+    the mask and writes y (sqr_conv2d_bwd_data_bn_act) before its weight gradient reads y.  Whatever
+    path needs y or the mask before that calls materialize() (one sqr_bn_apply pass)."""
+
+    __slots__ = ("x", "coef", "mask", "y", "y_written", "mask_written")
+
+    def __init__(self, x, coef, mask, y):
+        self.x, self.coef, self.mask, self.y = x, coef, mask, y
+        self.y_written = self.mask_written = False
+
+    def materialize(self):
+        if self.y_written and self.mask_written:
+            return
+        x = self.x
+        N, C, H, W = x.shape
+        y = self.y if not self.y_written else torch.empty_like(self.y, memory_format=_CL)
+        check(lib().sqr_bn_apply(ptr(x), ctypes.c_longlong(N * H * W), C, _dt(x), ptr(self.coef), None, 1, ptr(y),
+                                 ptr(self.mask), stream_ptr(x.device)), "sqr_bn_apply")
+        self.y_written = self.mask_written = True
 
 
 # BNActFn outputs whose apply pass was deferred to the consuming conv, by data pointer (handed to the
@@ -227,10 +261,7 @@ def apply_deferred(y):
     if pend is None:
         return
     del y._sqr_bnin
-    x, coef, mask = pend
-    N, C, H, W = x.shape
-    check(lib().sqr_bn_apply(ptr(x), ctypes.c_longlong(N * H * W), C, _dt(x), ptr(coef), None, 1, ptr(y), ptr(mask),
-                             stream_ptr(x.device)), "sqr_bn_apply")
+    pend.materialize()
 
 
 def _operand(x, stats, weight, bias, rmean, rvar, momentum, eps, mean, invstd):

@@ -8,6 +8,8 @@ torch/models.py:134-184).  Each forward packs the weight into the kernel layouts
 Compute dtype: bfloat16 / float16 when the input has that dtype or CUDA autocast is on with it,
 else float32 (exact-f32 MFMA: the parity mode).
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -205,8 +207,9 @@ def conv2d_fwd(x, w_krsc, d, return_ws=False, stats=False):
 
 def conv2d_fwd_bnin(x_pre, coef, x_act, mask, w_krsc, d):
     """(y, partials) of conv(relu(x_pre * scale + shift)) with the preceding BatchNorm applied while
-    the conv stages its input; x_act and mask receive that activation and its ReLU mask
-    (sqr_conv2d_fwd_stats_bnin).  None where the kernel does not take the shape (nothing written)."""
+    the conv stages its input; x_act and mask receive that activation and its ReLU mask, or are both
+    None: no side outputs (sqr_conv2d_fwd_stats_bnin).  None where the kernel does not take the shape
+    (nothing written)."""
     import ctypes
     ho, wo = _out_hw(d)
     dt = _TORCH_DT[d.dtype]
@@ -322,6 +325,35 @@ def conv2d_bwd_data_bn(gy, w_crsk, d, bn_x, bn_mask, bn_mean):
     return g, st[:rows.value * 2 * d.C].view(rows.value, 2, d.C)
 
 
+# A/B switch: 0 keeps the deferred BatchNorm output's side outputs (layer 1) / apply pass (layers 2-4)
+_BN_NSO = os.environ.get("SQR_BN_NSO", "1") != "0"
+
+
+def bnin_nso_supported(d):
+    """The conv of desc d can consume a deferred BatchNorm + ReLU output without it ever being written
+    in the forward (sqr_conv2d_bnin_nso_supported)."""
+    import ctypes
+    return _BN_NSO and bool(lib().sqr_conv2d_bnin_nso_supported(ctypes.byref(d)))
+
+
+def conv2d_bwd_data_bn_act(gy, w_crsk, d, bn_x, bn_coef, bn_mean, act_out):
+    """conv2d_bwd_data_bn for an input applied on load without side outputs: the ReLU mask is
+    recomputed from bn_x and the forward coefficients, and act_out receives the activation
+    (sqr_conv2d_bwd_data_bn_act)."""
+    import ctypes
+    dt = _TORCH_DT[d.dtype]
+    g = torch.empty((d.N, d.C, d.H, d.W), dtype=dt, device=gy.device, memory_format=_CL)
+    L = lib()
+    st = torch.empty(L.sqr_conv2d_bwd_data_bn_stats_floats(ctypes.byref(d)), dtype=torch.float32, device=gy.device)
+    rows = ctypes.c_int()
+    with _Probe("dgrad", d):
+        rc = L.sqr_conv2d_bwd_data_bn_act(ptr(gy), ptr(w_crsk), ptr(g), ptr(bn_x), ptr(bn_coef), ptr(bn_mean),
+                                          ptr(act_out), ptr(st), ctypes.byref(rows), ctypes.byref(d),
+                                          stream_ptr(gy.device))
+    check(rc, "sqr_conv2d_bwd_data_bn_act")
+    return g, st[:rows.value * 2 * d.C].view(rows.value, 2, d.C)
+
+
 class BnBackwardLink:
     """bn1 -> relu -> conv2 of a BasicBlock (torch/models.py:181): conv2's backward-data also
     produces bn1's backward reduction (sqr_conv2d_bwd_data_bn), so bn1's backward skips its own pass
@@ -330,10 +362,10 @@ class BnBackwardLink:
     consumer in a BasicBlock), otherwise it runs its own reduction (masking an already-masked g is
     harmless)."""
 
-    __slots__ = ("x", "mask", "mean", "invstd", "gamma", "pids", "g", "stats", "coef", "dgamma", "dbeta")
+    __slots__ = ("x", "mask", "mean", "invstd", "gamma", "pids", "g", "stats", "coef", "dgamma", "dbeta", "deferred")
 
     def __init__(self):
-        self.x = self.mask = self.mean = self.invstd = self.gamma = self.pids = None
+        self.x = self.mask = self.mean = self.invstd = self.gamma = self.pids = self.deferred = None
         self.g = self.stats = self.coef = self.dgamma = self.dbeta = None
 
     @staticmethod
@@ -353,7 +385,7 @@ class BnBackwardLink:
         got = (self.g, self.stats, self.coef, self.dgamma, self.dbeta)
         # the link is spent: drop every tensor it holds (the forward operands too)
         self.g = self.stats = self.coef = self.dgamma = self.dbeta = None
-        self.x = self.mask = self.mean = self.invstd = self.gamma = self.pids = None
+        self.x = self.mask = self.mean = self.invstd = self.gamma = self.pids = self.deferred = None
         g = got[0]
         if g is None or got[1] is None or dy.data_ptr() != g.data_ptr() or dy.shape != g.shape:
             return None
@@ -547,14 +579,20 @@ class Conv2dFn(torch.autograd.Function):
             krsc, crsk = pack_weight(weight, d, need_dx and C >= 8)
         stats = None
         fused = None
-        if pend is not None:  # apply-on-load: xin (= x) and the mask are written by the conv itself
-            x_pre, coef, mask = pend
+        ctx.deferred = None
+        if pend is not None:
+            x_pre, coef, mask = pend.x, pend.coef, pend.mask
+            # without side outputs: this conv's backward-data rebuilds the activation and its mask
+            # (the BnBackwardLink of the same BatchNorm), so neither is written in the forward
+            nso = bnb is not None and bnb.deferred is pend and need_dx and bnin_nso_supported(d)
             with _Probe("fwd_bnin", d):
-                fused = conv2d_fwd_bnin(x_pre, coef, xin, mask, krsc, d)
+                fused = conv2d_fwd_bnin(x_pre, coef, None if nso else xin, None if nso else mask, krsc, d)
             if fused is None:  # not this kernel's shape: the apply pass first
-                x._sqr_bnin = pend
-                from .bn import apply_deferred
-                apply_deferred(x)
+                pend.materialize()
+            elif nso:
+                ctx.deferred = pend
+            else:  # activation and mask written as side outputs
+                pend.y_written = pend.mask_written = True
         if fused is not None:
             (y, stats), ws = fused, None
         elif want_stats and bias is None:
@@ -614,7 +652,17 @@ class Conv2dFn(torch.autograd.Function):
                            and d.W % 2 == 0 and addend.t.is_contiguous(memory_format=_CL)):
                 addend, s2 = addend.full(), False
             link = ctx.bnb if (ctx.bnb is not None and ctx.bnb.ready() and addend is None) else None
-            if link is not None and link.x.dtype == dt:
+            deferred = ctx.deferred
+            if link is not None and link.x.dtype == dt and deferred is not None and link.deferred is deferred \
+                    and not deferred.y_written and (xin is None or xin.data_ptr() == deferred.y.data_ptr()):
+                # the input was applied on load without side outputs: the mask is recomputed here and
+                # the activation written for the weight gradient below
+                dx, link.stats = conv2d_bwd_data_bn_act(g, crsk, d, link.x, deferred.coef, link.mean, xin)
+                deferred.y_written = True
+                link.g = dx
+            elif link is not None and link.x.dtype == dt:
+                if deferred is not None:
+                    deferred.materialize()
                 dx, link.stats = conv2d_bwd_data_bn(g, crsk, d, link.x, link.mask, link.mean)
                 link.g = dx
             elif isinstance(addend, _MaskedDone):
@@ -645,6 +693,8 @@ class Conv2dFn(torch.autograd.Function):
                 if isinstance(dx, CompactS2):  # (not deposited: conv1's backward already ran)
                     dx = dx.full()
         if ctx.needs_input_grad[1]:
+            if ctx.deferred is not None and not ctx.deferred.y_written:
+                ctx.deferred.materialize()  # (no backward-data above wrote the activation)
             fin = None
             link = ctx.bnb
             if link is not None and link.stats is not None and link.g is not None and col is None \

@@ -79,3 +79,69 @@ def test_block_step_with_apply_on_load_equals_without(config):
         assert a["loss"] == b["loss"]
         for n in a["grads"]:
             assert torch.equal(a["grads"][n], b["grads"][n]), n
+
+
+# ---- apply-on-load without side outputs (the activation never written by the forward): the
+# forward (persistent layer-1 and tiled layer 2-4 kernels) and the backward-data launch that rebuilds
+# the activation and its mask, against the two-pass path, bitwise -- ResNetSQ's bn1 -> conv2 shapes at
+# 256^2 (B=64) and 512^2 input
+NSO_SHAPES = [(64, 64, 64), (64, 128, 32), (64, 256, 16), (64, 512, 8), (16, 64, 128), (64, 128, 64), (64, 256, 32),
+              (64, 512, 16)]
+
+
+def _nso_operands(N, C, H, dtype, seed):
+    from sqr import conv as sc
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x_pre = (torch.randn(N, C, H, H, device=DEV, generator=g) * 2 + 0.3).to(dtype).contiguous(
+        memory_format=torch.channels_last)
+    coef = torch.cat([torch.randn(C, device=DEV, generator=g) * 0.8, torch.randn(C, device=DEV, generator=g) * 0.5])
+    w = torch.randn(C, C, 3, 3, device=DEV, generator=g) / (3.0 * C ** 0.5)
+    d = sc._desc(N, C, H, H, C, 3, 3, 1, 1, dtype)
+    krsc, crsk = sc.pack_weight(w, d, True)
+    return g, x_pre, coef, d, krsc, crsk
+
+
+def _apply(x_pre, coef, dtype):
+    from sqr import conv as sc
+    from sqr._lib import check, lib, ptr, stream_ptr
+    N, C, H, W = x_pre.shape
+    M = N * H * W
+    a = torch.empty_like(x_pre)
+    m = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    check(lib().sqr_bn_apply(ptr(x_pre), ctypes.c_longlong(M), C, sc._DT[dtype], ptr(coef), None, 1, ptr(a), ptr(m),
+                             stream_ptr(torch.device(DEV))), "apply")
+    return a, m
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("N,C,H", NSO_SHAPES)
+def test_conv_bnin_no_side_outputs_equals_apply_then_conv(N, C, H, dtype):
+    from sqr import conv as sc
+    _, x_pre, coef, d, krsc, _ = _nso_operands(N, C, H, dtype, N * 13 + C + H)
+    assert sc.bnin_nso_supported(d)
+    a_ref, _ = _apply(x_pre, coef, dtype)
+    y_ref, s_ref = sc.conv2d_fwd(a_ref, krsc, d, stats=True)
+    y, s = sc.conv2d_fwd_bnin(x_pre, coef, None, None, krsc, d)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    assert s.shape == s_ref.shape and torch.equal(s, s_ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
+@pytest.mark.parametrize("N,C,H", NSO_SHAPES)
+def test_bwd_data_bn_act_equals_mask_path(N, C, H, dtype):
+    """The backward-data launch of the no-side-output path (mask recomputed from x and the
+    coefficients, activation written) against the mask-reading one on the apply pass's mask: g, the
+    BatchNorm backward partials and the activation bitwise."""
+    from sqr import conv as sc
+    g, x_pre, coef, d, _, crsk = _nso_operands(N, C, H, dtype, N * 17 + C + H)
+    gy = torch.randn(N, C, H, H, device=DEV, generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+    mean = torch.randn(C, device=DEV, generator=g) * 0.3
+    a_ref, m_ref = _apply(x_pre, coef, dtype)
+    g_ref, s_ref = sc.conv2d_bwd_data_bn(gy, crsk, d, x_pre, m_ref, mean)
+    act = torch.full_like(x_pre, float("nan"))
+    g2, s2 = sc.conv2d_bwd_data_bn_act(gy, crsk, d, x_pre, coef, mean, act)
+    torch.cuda.synchronize()
+    assert torch.equal(act, a_ref)
+    assert torch.equal(g2, g_ref)
+    assert s2.shape == s_ref.shape and torch.equal(s2, s_ref)

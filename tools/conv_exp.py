@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="64,64,64,64", help="N,C,H,K (3x3 conv, square images)")
     ap.add_argument("--stride", type=int, default=1)
-    ap.add_argument("--phase", default="fwd", choices=("fwd", "dgrad", "wgrad"))
+    ap.add_argument("--phase", default="fwd", choices=("fwd", "fwd_bnin", "dgrad", "dgrad_bnact", "wgrad"))
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--replays", type=int, default=5)
@@ -40,12 +40,18 @@ def main():
     w = torch.randn(K, C, 3, 3, device=dev, generator=g) / (9 * C) ** 0.5
     d = sc._desc(N, C, H, H, K, 3, 3, a.stride, 1, dt)
     krsc, crsk = sc.pack_weight(w, d, True)
+    coef = torch.cat([torch.randn(C, device=dev, generator=g) * 0.8, torch.randn(C, device=dev, generator=g) * 0.5])
+    act = torch.empty_like(x)
     clk = torch.empty(a.reps, 2, dtype=torch.int64, device=dev)
     add = torch.randn(N, C, H, H, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
 
     def one():
         if a.phase == "fwd":
             sc.conv2d_fwd(x, krsc, d, stats=True)
+        elif a.phase == "fwd_bnin":  # the preceding BatchNorm + ReLU applied on load, no side outputs
+            sc.conv2d_fwd_bnin(x, coef, None, None, krsc, d)
+        elif a.phase == "dgrad_bnact":  # backward-data rebuilding the BatchNorm mask and activation
+            sc.conv2d_bwd_data_bn_act(gy, crsk, d, x, coef, coef[:C], act)
         elif a.phase == "dgrad" and a.acc:
             sc.conv2d_bwd_data_acc(gy, crsk, d, add)
         elif a.phase == "dgrad":
@@ -61,7 +67,7 @@ def main():
         one()
     torch.cuda.current_stream().wait_stream(s)
     graph = torch.cuda.CUDAGraph()
-    sc.set_probe(a.phase, N, C, H, K, 3, a.stride, clock=clk)
+    sc.set_probe({"fwd_bnin": "fwd_bnin", "dgrad_bnact": "dgrad"}.get(a.phase, a.phase), N, C, H, K, 3, a.stride, clock=clk)
     with torch.cuda.graph(graph):
         for _ in range(a.reps):
             one()

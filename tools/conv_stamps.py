@@ -22,7 +22,8 @@ sys.path.insert(0, os.path.join(ROOT, "sq-recovery_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="64,128,32,128", help="N,C,H,K (3x3 conv, square images)")
-    ap.add_argument("--phase", default="fwd", choices=("fwd", "dgrad", "wgrad"))
+    ap.add_argument("--phase", default="fwd", choices=("fwd", "fwd_bnin", "dgrad", "dgrad_bnact", "wgrad"))
+    ap.add_argument("--stride", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16"))
     ap.add_argument("--maxwg", type=int, default=8192,
                     help="stamp buffer capacity: must equal SQR_STAMP_MAXWG of the stamps build (tools/build_stamps.sh)")
@@ -34,14 +35,21 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(N, C, H, H, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
-    gy = torch.randn(N, K, H, H, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
+    Ho = (H + 2 - 3) // a.stride + 1
+    gy = torch.randn(N, K, Ho, Ho, device=dev, generator=g).to(dt).contiguous(memory_format=torch.channels_last)
     w = torch.randn(K, C, 3, 3, device=dev, generator=g) / (9 * C) ** 0.5
-    d = sc._desc(N, C, H, H, K, 3, 3, 1, 1, dt)
+    d = sc._desc(N, C, H, H, K, 3, 3, a.stride, 1, dt)
     krsc, crsk = sc.pack_weight(w, d, True)
+    coef = torch.cat([torch.randn(C, device=dev, generator=g) * 0.8, torch.randn(C, device=dev, generator=g) * 0.5])
+    act = torch.empty_like(x)
 
     def one():
         if a.phase == "fwd":
             sc.conv2d_fwd(x, krsc, d, stats=True)
+        elif a.phase == "fwd_bnin":  # the preceding BatchNorm + ReLU applied on load, no side outputs
+            sc.conv2d_fwd_bnin(x, coef, None, None, krsc, d)
+        elif a.phase == "dgrad_bnact":  # backward-data rebuilding the BatchNorm mask and activation
+            sc.conv2d_bwd_data_bn_act(gy, crsk, d, x, coef, coef[:C], act)
         elif a.phase == "dgrad":
             sc.conv2d_bwd_data(gy, crsk, d)
         else:
@@ -52,7 +60,7 @@ def main():
     torch.cuda.synchronize()
     buf = torch.zeros(2 + 8 * a.maxwg, dtype=torch.int64, device=dev)
     buf[0] = -1
-    sc.set_probe(a.phase, N, C, H, K, 3, 1, clock=buf.view(-1, 2))
+    sc.set_probe({"fwd_bnin": "fwd_bnin", "dgrad_bnact": "dgrad"}.get(a.phase, a.phase), N, C, H, K, 3, a.stride, clock=buf.view(-1, 2))
     one()
     sc.set_probe(None, 0, 0, 0, 0, 0, 0)
     torch.cuda.synchronize()
@@ -67,7 +75,8 @@ def main():
     ph = np.diff(st, axis=1)  # prologue, first chunk, rest of the loop, epilogue
     q = lambda x, p: round(float(np.percentile(x, p)), 2)
     names = ["prologue", "chunk0", "loop_rest", "epilogue"]
-    out = {"shape": a.shape, "phase": a.phase, "lib": os.path.basename(os.path.dirname(LIB_PATH)), "workgroups": int(used.sum()),
+    out = {"shape": a.shape, "stride": a.stride, "phase": a.phase,
+           "env": {k: v for k, v in os.environ.items() if k.startswith("SQR_") and k != "SQR_LIB"}, "lib": os.path.basename(os.path.dirname(LIB_PATH)), "workgroups": int(used.sum()),
            "span_us": round(float(st[:, 4].max()), 2),
            "start_us": {"p50": q(st[:, 0], 50), "p90": q(st[:, 0], 90), "max": q(st[:, 0], 100)},
            "end_us": {"min": q(st[:, 4], 0), "p50": q(st[:, 4], 50), "max": q(st[:, 4], 100)}}
