@@ -188,10 +188,12 @@ int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_c
 int sqr_conv2d_fwd_stats_bnin(const void* x_pre, const float* coef, void* x_act, uint8_t* x_mask,
                               const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats, int* stats_rows,
                               void* stream);
-/* 1 if conv d (C -> K) as the consumer of a BatchNorm + ReLU runs without the activation in memory:
- * sqr_conv2d_fwd_stats_bnin with x_act = x_mask = NULL and sqr_conv2d_bwd_data_bn_act are both
- * handled by direct kernels at this shape (16-bit 3x3 / s1 / p1; ResNetSQ's layer 1-4 convs at 256^2
- * and 512^2 input and batch 64), else 0. */
+/* 1 if conv d (C -> K) as the consumer of a BatchNorm + ReLU should run without the activation in
+ * memory: sqr_conv2d_fwd_stats_bnin with x_act = x_mask = NULL and sqr_conv2d_bwd_data_bn_act are
+ * handled by direct kernels at this shape AND that beats the apply pass (side outputs) there --
+ * ResNetSQ's layer-2/3 convs at 256^2 input, layers 2-4 at 512^2, batch 64.  sqr_conv2d_fwd_stats_bnin
+ * without side outputs also takes the persistent layer-1 shapes, and both entry points the 8x8
+ * layer-4 tiles; the query answers 0 there (the side-output / apply-pass path is faster). */
 int sqr_conv2d_bnin_nso_supported(const sqr_conv_desc* d);
 /* dy [N,Ho,Wo,K], w_crsk (see pack_weight) -> dx [N,H,W,C]; strided convs run one stride-1
  * implicit GEMM per output-parity class (no work on structurally zero taps), all classes in one
@@ -234,8 +236,8 @@ int sqr_conv2d_bwd_data_bn(const void* dy, const void* w_crsk, void* g_out, cons
  * sqr_conv2d_fwd_stats_bnin with x_act = x_mask = NULL): the ReLU mask is recomputed from bn_x and the
  * forward coefficients bn_coef = [scale C][shift C] (the rounded activation > 0, as sqr_bn_apply forms
  * it), and act_out (nullable) receives the activation relu(bn_x * scale + shift) itself -- bitwise what
- * sqr_bn_apply writes -- for the conv's weight gradient.  Direct kernels only (the shapes of
- * sqr_conv2d_bnin_nso_supported): SQR_E_UNSUPPORTED otherwise. */
+ * sqr_bn_apply writes -- for the conv's weight gradient.  Tiled direct kernels only (not the
+ * persistent layer-1 shapes): SQR_E_UNSUPPORTED otherwise, nothing launched. */
 int sqr_conv2d_bwd_data_bn_act(const void* dy, const void* w_crsk, void* g_out, const void* bn_x,
                                const float* bn_coef, const float* bn_mean, void* act_out, float* stats,
                                int* stats_rows, const sqr_conv_desc* d, void* stream);

@@ -725,13 +725,11 @@ struct D3PArgs {
   const void* bn_x;        // BNB launches: the following BatchNorm's input x [N][H][TW][64] ...
   const uint8_t* bn_mask;  // ... its ReLU mask (1 bit / element) and ...
   const float* bn_mean;    // ... its batch mean: out = dgrad * mask, stats = its backward sums
-  const float* bn_coef;    // BNB, nullable: mask recomputed from bn_x and the forward [2][64] (scale, shift)
-  void* bn_act;            // BNB with bn_coef, nullable: the activation relu(bn_x * scale + shift) written here
   float* stats;    // nullable: BatchNorm partials [gridDim.x][2][64]
   const float* in_coef;  // BNIN launches: x is the PRE-activation of the preceding BatchNorm + ReLU,
   void* in_act;          // [2][64] its (scale, shift): the conv reads relu(x * scale + shift) and writes
   uint8_t* in_mask;      // that activation (in_act) and its ReLU mask (1 bit / element) as side outputs
-                         // (both null: no side outputs -- the BNB dgrad of the backward rebuilds them)
+                         // (both null: no side outputs, y and the statistics only)
   int H, bpi, tpb, flip;  // bands per image, 2-row tiles per band
   uint32_t xbytes, wbytes;
   unsigned long long* tp;  // nullable: clock probe slots
@@ -809,8 +807,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     const int lbase = ((row + 1) & (NSLOT - 1)) * SLOTR + part * 8;  // first LDS row of the piece
     const int L = lbase + prow, w = part * 8 + prow - 1;
     const bool ok = use && (unsigned)row < (unsigned)H && (unsigned)w < (unsigned)TW;
-    *vo = ok ? (uint32_t)((((img * H + row) * TW + w) * C) * 2 + ((pslot ^ ((L >> 1) & 7)) << 4)) : kOOB;
-    return lbase * ROWB + lane * 16;
+    // the lane fetches channel group pslot and writes it to the swizzled slot pslot ^ key(L): the same
+    // LDS image as a fetch of the swizzled group into slot pslot, but every piece a lane handles holds
+    // the same 8 channels (BNIN keeps their coefficients in registers)
+    *vo = ok ? (uint32_t)((((img * H + row) * TW + w) * C) * 2 + (pslot << 4)) : kOOB;
+    return L * ROWB + ((pslot ^ ((L >> 1) & 7)) << 4);
   };
   auto load_rows = [&](int r0, int nrows, u32x4* v, bool use) {  // every wave issues the same count
 #pragma unroll
@@ -840,24 +841,21 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     }
   };
 
+  float isc[BNIN ? 8 : 1], ish[BNIN ? 8 : 1];  // BNIN: (scale, shift) of channels 8 pslot .. +7
   // BNIN: piece p of the nrows rows from r0 (the lane's 16 B of it, as row_piece maps them) ->
   // relu(v * scale + shift) in place; the band's own rows also go out as the activation + mask
   auto bn_in_piece = [&](int r0, int nrows, int p, u32x4& v) {
     if constexpr (BNIN) {
       const int j = p / PPR, part = p - j * PPR;
       const int row = r0 + j;
-      const int L = ((row + 1) & (NSLOT - 1)) * SLOTR + part * 8 + prow, w = part * 8 + prow - 1;
+      const int w = part * 8 + prow - 1;
       if (p < nrows * PPR && (unsigned)row < (unsigned)H && (unsigned)w < (unsigned)TW) {
-        const int cg = pslot ^ ((L >> 1) & 7);  // the 8 channels this lane's piece holds
-        const f32x4 s0 = *(const f32x4*)(bnc + 8 * cg), s1 = *(const f32x4*)(bnc + 8 * cg + 4);
-        const f32x4 t0 = *(const f32x4*)(bnc + 64 + 8 * cg), t1 = *(const f32x4*)(bnc + 64 + 8 * cg + 4);
+        const int cg = pslot;  // the 8 channels every piece of this lane holds (row_piece)
         uint32_t mb = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float sc0 = e < 2 ? s0[2 * e] : s1[2 * e - 4], sc1 = e < 2 ? s0[2 * e + 1] : s1[2 * e - 3];
-          const float sh0 = e < 2 ? t0[2 * e] : t1[2 * e - 4], sh1 = e < 2 ? t0[2 * e + 1] : t1[2 * e - 3];
-          const float o0 = fmaxf(fmaf(lo2f<T>(v[e]), sc0, sh0), 0.f);
-          const float o1 = fmaxf(fmaf(hi2f<T>(v[e]), sc1, sh1), 0.f);
+          const float o0 = fmaxf(fmaf(lo2f<T>(v[e]), isc[2 * e], ish[2 * e]), 0.f);
+          const float o1 = fmaxf(fmaf(hi2f<T>(v[e]), isc[2 * e + 1], ish[2 * e + 1]), 0.f);
           v[e] = pack2<T>(o0, o1);
           mb |= (lo2f<T>(v[e]) > 0.f ? 1u : 0u) << (2 * e);
           mb |= (hi2f<T>(v[e]) > 0.f ? 1u : 0u) << (2 * e + 1);
@@ -887,15 +885,7 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
   u32x4 av[NST];  // ACC: the addend pieces of the tile stored next; BNB: the BatchNorm input x there
   uint32_t bm[(BNB || ACC) ? NST : 1];  // BNB / masked ACC: the mask byte of each piece (8 channels)
   float bs1[BNB ? 8 : 1], bs2[BNB ? 8 : 1], bmu[BNB ? 8 : 1];  // BNB: this thread's 8 channels (tid & 7)
-  float bsc[BNB ? 8 : 1], bsh[BNB ? 8 : 1];  // BNB with bn_coef: their forward (scale, shift)
-  const bool bcoef = BNB && a.bn_coef != nullptr;
   if constexpr (BNB) {
-    const float* cp = bcoef ? a.bn_coef : a.bn_mean;  // (a valid pointer either way: no load behind a test)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      bsc[e] = cp[(tid & 7) * 8 + e];
-      bsh[e] = cp[(bcoef ? 64 : 0) + (tid & 7) * 8 + e];
-    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       bs1[e] = bs2[e] = 0.f;
@@ -906,18 +896,13 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     const size_t tile0 = ((size_t)img * H + hb + k * TH) * TW * BN;  // first element of tile k
     const char* src = (const char*)(BNB ? a.bn_x : a.addend) + tile0 * 2;
     av[q] = *(const u32x4*)(src + (size_t)(q * NT + tid) * 16);
-    if constexpr (BNB) bm[q] = bcoef ? 0u : a.bn_mask[tile0 / 8 + q * NT + tid];
+    if constexpr (BNB) bm[q] = a.bn_mask[tile0 / 8 + q * NT + tid];
     if constexpr (ACC) bm[q] = a.addend_mask ? a.addend_mask[tile0 / 8 + q * NT + tid] : 0xffu;
   };
   // (use = false: a tile that does not exist -- the stores go out of the buffer's range and are
   // dropped; issuing them anyway keeps the vector-memory instruction count the same on every path,
   // so the compiler's vmcnt waits for the row registers never include these stores)
   const __amdgpu_buffer_rsrc_t osrd = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.xbytes, 0x00020000);
-  // BNB: the activation output (a store is issued for every piece either way -- out of range when
-  // there is none -- so that every path has the same vector-memory instruction count)
-  const bool bact = BNB && bcoef && a.bn_act != nullptr;
-  const __amdgpu_buffer_rsrc_t asrd =
-      __builtin_amdgcn_make_buffer_rsrc(bact ? a.bn_act : a.out, 0, a.xbytes, 0x00020000);
   auto store_piece = [&](int k, bool use, int q) {
     const uint32_t dst = use ? (uint32_t)(((img * H + hb + k * TH) * TW * BN) * 2) : kOOB;
     {
@@ -950,22 +935,9 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
         }
       }
       if constexpr (BNB) {
-        uint32_t mbyte = bm[q];
-        u32x4 act = {0u, 0u, 0u, 0u};
-        if (bcoef) {  // the activation and its mask, exactly as the apply pass forms them
-          mbyte = 0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            act[e] = pack2<T>(fmaxf(fmaf(lo2f<T>(av[q][e]), bsc[2 * e], bsh[2 * e]), 0.f),
-                              fmaxf(fmaf(hi2f<T>(av[q][e]), bsc[2 * e + 1], bsh[2 * e + 1]), 0.f));
-            mbyte |= (lo2f<T>(act[e]) > 0.f ? 1u : 0u) << (2 * e);
-            mbyte |= (hi2f<T>(act[e]) > 0.f ? 1u : 0u) << (2 * e + 1);
-          }
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(act, asrd, (use && bact ? dst : kOOB) | (uint32_t)(c * 16), 0, 0);
 #pragma unroll
         for (int e = 0; e < 4 && use; ++e) {
-          const uint32_t keep = (((mbyte >> (2 * e)) & 1u) ? 0xffffu : 0u) | (((mbyte >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u);
+          const uint32_t keep = (((bm[q] >> (2 * e)) & 1u) ? 0xffffu : 0u) | (((bm[q] >> (2 * e + 1)) & 1u) ? 0xffff0000u : 0u);
           v[e] &= keep;  // g = dgrad * mask (masked halves become +0)
           const float g0 = lo2f<T>(v[e]), g1 = hi2f<T>(v[e]);
           bs1[2 * e] += g0;
@@ -1007,6 +979,11 @@ __global__ void __launch_bounds__(256) conv3p_kernel(D3PArgs a) {
     }
     if constexpr (BNIN) {
       __syncthreads();  // the coefficients
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        isc[e] = bnc[8 * pslot + e];
+        ish[e] = bnc[64 + 8 * pslot + e];
+      }
 #pragma unroll
       for (int i = 0; i < PRW; ++i)
         if (i * NW + NW <= (TH + 2) * PPR || i * NW + wave < (TH + 2) * PPR) bn_in_piece(hb - 1, TH + 2, i * NW + wave, t0[i]);
@@ -1962,12 +1939,18 @@ bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
 bool bnin_tiled_id(int id) { return id == 7 || id == 8 || id == 10; }
 constexpr int kBninMaxC = 512;  // conv3_kernel's BNIN coefficient table
 
+// Where the no-side-output path is also the faster one (config-2 step tables, profiles/r06e_c2_steps.txt
+// against r06a_c2_steps.txt, per BasicBlock): the tiled 32- and 16-wide tiles (ids 7, 8) save the
+// apply pass for +1.2 / +1.3 us on the forward (layers 2 and 3: -4 / -5 us per block).  Not the
+// persistent layer-1 kernel (its side outputs cost the forward +12 us, the activation store the
+// backward-data +9.4 us) nor the two-image 8x8 tiles (id 10: the window transform and the loss of the
+// k20 key cost +7.4 us, more than layer 4's small apply pass).
 int conv3_bnin_nso_ok(int N, int H, int W, int C, int K) {
-  if (g_direct == 0 || C % 64 || K % 64 || pow2_log(W) < 0) return 0;
-  if (C == 64 && K == 64 && (W == 64 || W == 128) && H % (W == 64 ? 2 : 1) == 0 && g_persist) return 1;
+  if (g_direct == 0 || C % 64 || K % 64 || pow2_log(W) < 0 || C > kBninMaxC) return 0;
+  if (C == 64 && K == 64 && (W == 64 || W == 128) && H % (W == 64 ? 2 : 1) == 0 && g_persist) return 0;
   D3Cfg f, b;
   // the forward (C -> K, BNIN) and the backward-data (K -> C, BNB with coefficients) both direct
-  return C <= kBninMaxC && pick(N, H, W, C, K, &f) && bnin_tiled_id(f.id) && pick(N, H, W, K, C, &b) ? 1 : 0;
+  return pick(N, H, W, C, K, &f) && (f.id == 7 || f.id == 8) && pick(N, H, W, K, C, &b) ? 1 : 0;
 }
 
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
@@ -1981,6 +1964,8 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     if (bnin->act && !persist_shape) return kNotHandled;
   }
   if (bnb && bnb->act && !bnb->coef) return kNotHandled;  // the activation output needs the coefficients
+  // the mask from the coefficients: the tiled kernels only (layer-1 bn1 keeps the forward's side outputs)
+  if (bnb && bnb->coef && persist_shape) return kNotHandled;
   if (g_direct == 0) return kNotHandled;
   if (stride == 2) {  // forward only (H, W: the input size)
     if (flip || addend || bnb || H % 2 || W % 2 || Cin % 64 || Nout % 64) return kNotHandled;
@@ -2062,8 +2047,6 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
     p.bn_x = bnb ? bnb->x : nullptr;
     p.bn_mask = bnb ? bnb->mask : nullptr;
     p.bn_mean = bnb ? bnb->mean : nullptr;
-    p.bn_coef = bnb ? bnb->coef : nullptr;
-    p.bn_act = bnb ? bnb->act : nullptr;
     p.stats = stats;
     p.in_coef = bnin ? bnin->coef : nullptr;
     p.in_act = bnin ? bnin->act : nullptr;

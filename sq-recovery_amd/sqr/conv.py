@@ -217,8 +217,9 @@ def conv2d_fwd_bnin(x_pre, coef, x_act, mask, w_krsc, d):
     L = lib()
     st = torch.empty(L.sqr_conv2d_stats_floats(ctypes.byref(d)), dtype=torch.float32, device=x_pre.device)
     rows = ctypes.c_int()
-    rc = L.sqr_conv2d_fwd_stats_bnin(ptr(x_pre), ptr(coef), ptr(x_act), ptr(mask), ptr(w_krsc), ptr(y), ctypes.byref(d),
-                                     ptr(st), ctypes.byref(rows), stream_ptr(x_pre.device))
+    with _Probe("fwd_bnin", d):
+        rc = L.sqr_conv2d_fwd_stats_bnin(ptr(x_pre), ptr(coef), ptr(x_act), ptr(mask), ptr(w_krsc), ptr(y),
+                                         ctypes.byref(d), ptr(st), ctypes.byref(rows), stream_ptr(x_pre.device))
     if rc == -2:  # SQR_E_UNSUPPORTED
         return None
     check(rc, "sqr_conv2d_fwd_stats_bnin")
@@ -585,8 +586,7 @@ class Conv2dFn(torch.autograd.Function):
             # without side outputs: this conv's backward-data rebuilds the activation and its mask
             # (the BnBackwardLink of the same BatchNorm), so neither is written in the forward
             nso = bnb is not None and bnb.deferred is pend and need_dx and bnin_nso_supported(d)
-            with _Probe("fwd_bnin", d):
-                fused = conv2d_fwd_bnin(x_pre, coef, None if nso else xin, None if nso else mask, krsc, d)
+            fused = conv2d_fwd_bnin(x_pre, coef, None if nso else xin, None if nso else mask, krsc, d)
             if fused is None:  # not this kernel's shape: the apply pass first
                 pend.materialize()
             elif nso:

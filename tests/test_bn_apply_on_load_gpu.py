@@ -83,8 +83,8 @@ def test_block_step_with_apply_on_load_equals_without(config):
 
 # ---- apply-on-load without side outputs (the activation never written by the forward): the
 # forward (persistent layer-1 and tiled layer 2-4 kernels) and the backward-data launch that rebuilds
-# the activation and its mask, against the two-pass path, bitwise -- ResNetSQ's bn1 -> conv2 shapes at
-# 256^2 (B=64) and 512^2 input
+# the activation and its mask (tiled layers 2-4; layer 1 keeps the forward's side outputs), against
+# the two-pass path, bitwise -- ResNetSQ's bn1 -> conv2 shapes at 256^2 (B=64) and 512^2 input
 NSO_SHAPES = [(64, 64, 64), (64, 128, 32), (64, 256, 16), (64, 512, 8), (16, 64, 128), (64, 128, 64), (64, 256, 32),
               (64, 512, 16)]
 
@@ -118,7 +118,6 @@ def _apply(x_pre, coef, dtype):
 def test_conv_bnin_no_side_outputs_equals_apply_then_conv(N, C, H, dtype):
     from sqr import conv as sc
     _, x_pre, coef, d, krsc, _ = _nso_operands(N, C, H, dtype, N * 13 + C + H)
-    assert sc.bnin_nso_supported(d)
     a_ref, _ = _apply(x_pre, coef, dtype)
     y_ref, s_ref = sc.conv2d_fwd(a_ref, krsc, d, stats=True)
     y, s = sc.conv2d_fwd_bnin(x_pre, coef, None, None, krsc, d)
@@ -128,7 +127,7 @@ def test_conv_bnin_no_side_outputs_equals_apply_then_conv(N, C, H, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "f16"])
-@pytest.mark.parametrize("N,C,H", NSO_SHAPES)
+@pytest.mark.parametrize("N,C,H", [s for s in NSO_SHAPES if s[1] != 64])
 def test_bwd_data_bn_act_equals_mask_path(N, C, H, dtype):
     """The backward-data launch of the no-side-output path (mask recomputed from x and the
     coefficients, activation written) against the mask-reading one on the apply pass's mask: g, the
@@ -145,3 +144,25 @@ def test_bwd_data_bn_act_equals_mask_path(N, C, H, dtype):
     assert torch.equal(act, a_ref)
     assert torch.equal(g2, g_ref)
     assert s2.shape == s_ref.shape and torch.equal(s2, s_ref)
+
+
+def test_bnin_nso_query_picks_the_faster_path():
+    """sqr_conv2d_bnin_nso_supported: the tiled 32/16-wide tiles take the no-side-output path, the
+    persistent layer-1 kernel and the 8x8 layer-4 tiles keep theirs (BatchNorm)."""
+    from sqr import conv as sc
+    want = {(64, 64, 64): False, (64, 128, 32): True, (64, 256, 16): True, (64, 512, 8): False,
+            (16, 64, 128): False, (64, 128, 64): True, (64, 256, 32): True, (64, 512, 16): True}
+    for (N, C, H), on in want.items():
+        d = sc._desc(N, C, H, H, C, 3, 3, 1, 1, torch.bfloat16)
+        assert sc.bnin_nso_supported(d) == on, (N, C, H)
+
+
+def test_bwd_data_bn_act_declines_layer1():
+    """The persistent layer-1 shapes keep the forward's side outputs: the coefficient-mode
+    backward-data is not offered there (SQR_E_UNSUPPORTED, nothing launched)."""
+    from sqr import conv as sc
+    from sqr._lib import SqrError
+    _, x_pre, coef, d, _, crsk = _nso_operands(64, 64, 64, torch.bfloat16, 5)
+    gy = torch.zeros_like(x_pre)
+    with pytest.raises(SqrError):
+        sc.conv2d_bwd_data_bn_act(gy, crsk, d, x_pre, coef, coef[:64], torch.empty_like(x_pre))
