@@ -175,6 +175,10 @@ size_t sqr_conv2d_stats_floats(const sqr_conv_desc* d);
  * whenever it tiles), 2 whenever the shape tiles, 0 never (implicit-GEMM kernel for every shape).  Returns the previous mode.
  * Process-wide; meant for A/B tests. */
 int sqr_conv_set_direct(int mode);
+/* Tile choice of the tiled direct 3x3 kernels (layers 2-4): 1 = the deep weight rings (4- / 6- /
+ * 9-stage), 0 = the same tiles with 3-stage rings.  Returns the previous setting.  Process-wide; meant
+ * for A/B tests (results are bitwise the same: only the DMA pipelining differs). */
+int sqr_conv_set_deep_ring(int on);
 int sqr_conv2d_fwd_stats(const void* x, const void* w_krsc, void* y, const sqr_conv_desc* d, float* stats,
                          int* stats_rows, void* workspace, size_t workspace_bytes, void* stream);
 /* sqr_conv2d_fwd_stats of x_act = relu(x_pre * scale + shift), the preceding BatchNorm + ReLU applied

@@ -1776,6 +1776,7 @@ int env_int(const char* n, int dflt) {
 }
 #endif
 int g_persist = 1;  // layer-1 persistent kernel (0: the tiled conv3_kernel; tests compare the two)
+int g_deep_ring = 1;  // 1: the deep-weight-ring tiles (ids 7, 8, 10) first; 0: their 3-stage twins (1, 2, 5)
 
 
 int pow2_log(int x) {
@@ -1815,6 +1816,7 @@ bool pick(int N, int H, int W, int Cin, int Nout, D3Cfg* out) {
 #endif
   for (const D3Cfg& c : cands) {
     if (force >= 0 && c.id != force) continue;
+    if (force < 0 && !g_deep_ring && (c.id == 7 || c.id == 8 || c.id == 10)) continue;
     if (c.id == 0 && !(Nout == 64 && nch == 1)) continue;
     if (c.id != 0 && Nout % c.BN) continue;
     if (W % c.TW || H % c.TH) continue;
@@ -1882,6 +1884,29 @@ int conv3s2_dgrad_launch(int dtype, const void* dy, const void* w_cls, const int
   // slower
   const dim3 grid(N * a.tiles_per_img * a.ntn);
   probe_begin(st);
+#ifdef SQR_EXPERIMENTS
+  static const int xpd = env_int("SQR_S2D_PD", 0);  // experiment builds: another weight-ring depth
+  if (xpd == 2 || xpd == 3 || xpd == 5) {
+    SQR_DISPATCH16(dtype, T, {
+      if (nch == 2) {
+        if (xpd == 2) hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 32, 64, 4, 2, 2, 2>), grid, dim3(512), 0, st, a);
+        else if (xpd == 3) hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 32, 64, 4, 2, 2, 3>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 32, 64, 4, 2, 2, 5>), grid, dim3(512), 0, st, a);
+      } else if (nch == 8) {
+        if (xpd == 2) hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 8, 64, 2, 2, 8, 2>), grid, dim3(256), 0, st, a);
+        else if (xpd == 3) hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 8, 64, 2, 2, 8, 3>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 8, 64, 2, 2, 8, 5>), grid, dim3(256), 0, st, a);
+      } else {
+        if (xpd == 2) hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 4, 16, 64, 2, 2, 4, 2>), grid, dim3(256), 0, st, a);
+        else if (xpd == 3) hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 4, 16, 64, 2, 2, 4, 3>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 4, 16, 64, 2, 2, 4, 5>), grid, dim3(256), 0, st, a);
+      }
+    });
+    probe_end(st);
+    SQR_HIP_LAUNCH_CHECK("conv3s2_dgrad_kernel");
+    return 0;
+  }
+#endif
   SQR_DISPATCH16(dtype, T, {
     if (nch == 2)
       hipLaunchKernelGGL((conv3s2_dgrad_kernel<T, 8, 32, 64, 4, 2, 2, 5>), grid, dim3(512), 0, st, a);
@@ -1936,7 +1961,7 @@ bool pick_s2f(int N, int Ho, int Wo, int Cin, int Nout, D3S2FCfg* out) {
 }  // namespace
 
 // tiled configurations with an apply-on-load (BNIN) instantiation
-bool bnin_tiled_id(int id) { return id == 7 || id == 8 || id == 10; }
+bool bnin_tiled_id(int id) { return id == 7 || id == 8 || id == 10 || id == 1 || id == 2 || id == 5; }
 constexpr int kBninMaxC = 512;  // conv3_kernel's BNIN coefficient table
 
 // Where the no-side-output path is also the faster one (config-2 step tables, profiles/r06e_c2_steps.txt
@@ -1950,7 +1975,9 @@ int conv3_bnin_nso_ok(int N, int H, int W, int C, int K) {
   if (C == 64 && K == 64 && (W == 64 || W == 128) && H % (W == 64 ? 2 : 1) == 0 && g_persist) return 0;
   D3Cfg f, b;
   // the forward (C -> K, BNIN) and the backward-data (K -> C, BNB with coefficients) both direct
-  return pick(N, H, W, C, K, &f) && (f.id == 7 || f.id == 8) && pick(N, H, W, K, C, &b) ? 1 : 0;
+  return pick(N, H, W, C, K, &f) && (f.id == 7 || f.id == 8 || f.id == 1 || f.id == 2) && pick(N, H, W, K, C, &b)
+             ? 1
+             : 0;
 }
 
 int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int H, int W, int Cin, int Nout, int flip,
@@ -2149,8 +2176,11 @@ int conv3_launch(int dtype, const void* x, const void* w, void* out, int N, int 
       // apply-on-load instantiations: the first-choice tiles of ResNetSQ's layers 2-4 at 256 / 512 input
       switch (c.id) {
         // (id 7's tile with the 3-stage ring: the 4-stage one fills the 160 KiB without the table)
+        case 1:
         case 7: hipLaunchKernelGGL((conv3_kernel<T, 256, 128, 4, 2, 32, 8, 2, 1, 2, false, false, 1, true>), grid, blk, 0, st, a); break;
+        case 2: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 2, false, false, 1, true>), grid, blk, 0, st, a); break;
         case 8: hipLaunchKernelGGL((conv3_kernel<T, 128, 128, 4, 2, 16, 8, 2, 1, 5, false, false, 1, true>), grid, blk, 0, st, a); break;
+        case 5: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 2, false, false, 1, true>), grid, blk, 0, st, a); break;
         default: hipLaunchKernelGGL((conv3_kernel<T, 128, 64, 2, 2, 8, 8, 2, 2, 8, false, false, 1, true>), grid, blk, 0, st, a); break;
       }
     } else if (bnb) {
@@ -2262,6 +2292,12 @@ int conv3w_launch(int dtype, const void* x, const void* dy, float* slab, size_t 
 
 }  // namespace conv
 }  // namespace sqr
+
+extern "C" int sqr_conv_set_deep_ring(int on) {
+  const int old = sqr::conv::g_deep_ring;
+  sqr::conv::g_deep_ring = on ? 1 : 0;
+  return old;
+}
 
 extern "C" int sqr_conv_set_direct(int mode) {
   const int old = sqr::conv::g_direct;

@@ -92,6 +92,7 @@ SIGNATURES = {
     "sqr_conv2d_fwd": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p, c_size_t,
                                c_void_p]),
     "sqr_conv_set_direct": (c_int, [c_int]),
+    "sqr_conv_set_deep_ring": (c_int, [c_int]),
     "sqr_conv2d_stats_floats": (c_size_t, [ctypes.POINTER(SqrConvDesc)]),
     "sqr_conv2d_fwd_stats": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.POINTER(SqrConvDesc), c_void_p,
                                      ctypes.POINTER(c_int), c_void_p, c_size_t, c_void_p]),
@@ -213,6 +214,8 @@ def lib():
             fn = getattr(h, name)  # AttributeError = library/header mismatch: fail loudly
             fn.restype = res
             fn.argtypes = args
+        if os.environ.get("SQR_D3_DEEP") in ("0", "1"):  # A/B switch (sqr_conv_set_deep_ring)
+            h.sqr_conv_set_deep_ring(int(os.environ["SQR_D3_DEEP"]))
         _lib = h
     return _lib
 
